@@ -1,0 +1,73 @@
+"""ctypes binding of libf16env.so (the HIP product path).
+
+The library is built in-tree (f16_jsb_amd/libf16env.so, see build.py). torch is imported
+first so that the process has exactly one HIP runtime (torch's libamdhip64.so.7, which
+libf16env.so's NEEDED entry then resolves to). There is no CPU fallback: if the library is
+missing, or no GPU is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from .abi import EnvConfig
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libf16env.so")
+
+_lib = None
+
+
+class F16EnvError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libf16env.so (raises F16EnvError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- one HIP runtime per process (torch's)
+
+    if not os.path.exists(LIB_PATH):
+        raise F16EnvError(
+            "libf16env.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `python -m f16_jsb_amd.build`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
+    L.f16env_config_default.argtypes = [ctypes.POINTER(EnvConfig)]
+    L.f16env_create.argtypes = [ctypes.POINTER(EnvConfig), i32, ctypes.POINTER(vp)]
+    L.f16env_destroy.argtypes = [vp]
+    L.f16env_state_bytes.argtypes = [vp]
+    L.f16env_state_bytes.restype = sz
+    L.f16env_state_bytes_per_env.restype = i32
+    L.f16env_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.f16env_step.argtypes = [vp] * 13
+    L.f16env_get_state.argtypes = [vp, vp, vp]
+    L.f16env_set_state.argtypes = [vp, vp, vp]
+    L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
+    L.f16env_sample_actions.argtypes = [vp, vp, u64, u64, vp]
+    L.f16env_step_kernel_name.restype = ctypes.c_char_p
+    L.f16env_algorithmic_bytes_per_env_step.argtypes = [i32]
+    L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
+    L.f16env_last_error.restype = ctypes.c_char_p
+    for name in ("f16env_config_default", "f16env_create", "f16env_destroy", "f16env_reset",
+                 "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
+                 "f16env_sample_actions"):
+        getattr(L, name).restype = i32
+    _lib = L
+    return L
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = lib().f16env_last_error()
+        raise F16EnvError("%s failed (%d): %s" % (what, status, msg.decode() if msg else "?"))
+
+
+# symbols include/f16env.h declares (tests check the .so exports every one of them)
+EXPORTED_SYMBOLS = (
+    "f16env_config_default", "f16env_create", "f16env_destroy", "f16env_state_bytes",
+    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_get_state",
+    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_step_kernel_name",
+    "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
+)

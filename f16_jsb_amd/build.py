@@ -1,0 +1,43 @@
+"""In-tree build of libf16env.so for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m f16_jsb_amd.build [--verbose]
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "f16env.hip")
+OUT = os.path.join(HERE, "libf16env.so")
+DEPS = [SRC, os.path.join(HERE, "csrc", "f16_device.h"), os.path.join(HERE, "csrc", "f16_tables.h"),
+        os.path.join(ROOT, "include", "f16env.h")]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def build(verbose: bool = False, force: bool = False, extra=()) -> str:
+    if not force and os.path.exists(OUT):
+        t_out = os.path.getmtime(OUT)
+        if all(os.path.getmtime(d) <= t_out for d in DEPS):
+            return OUT
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
+           SRC, "-o", OUT + ".tmp", *extra]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv))

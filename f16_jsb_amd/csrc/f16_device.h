@@ -1,0 +1,811 @@
+// f16_device.h -- per-lane F-16 flight dynamics for CDNA4 (gfx950), one lane per env.
+//
+// The path restated here is the one behind jsbsim.FGFDMExec.run() in the reference
+// (jsbsim_gym/jsbsim_gym.py:225-232): FCS (aircraft/f16/f16.xml:309-984), FGTurbine
+// (Engines/F100-PW-229.xml), aerodynamics (f16.xml:986-1917), US-1976 atmosphere, WGS84/J2
+// gravity, 6-DoF equations of motion with JSBSim's default integrators. The CPU oracle
+// (oracle/f16ref.c) is the readable fp64 statement of the same algorithm; this file is the
+// fp32 register-resident version with fp64 kept only where fp32 cannot hold the precision
+// (ECI position/velocity at |r| ~ 2.1e7 ft, the Earth rotation angle and the geodetic
+// altitude). Tables live in LDS (f16_tables.h blob, grouped by shared breakpoint vectors);
+// breakpoints are compile-time literals.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/f16env.h"
+#include "f16_tables.h"
+
+namespace f16 {
+
+// ------------------------------------------------------------------------------------------
+// constants shared with the host (filled by f16env_create from the same formulas as the
+// oracle's init_consts(), in double, then stored in the kernel argument block)
+// ------------------------------------------------------------------------------------------
+struct ModelConsts {
+  float inv_mass;            // 1/slug
+  float J[9], Jinv[9];       // body inertia, slug ft^2
+  float rp[3], eye[3], eng[3];  // AERORP / EYEPOINT / thruster rel. CG (body ft)
+  float inv_gref;            // 1 / (GM/a^2)
+  float rho_sl, a_sl, p_sl;  // US-76 sea level (slug/ft3, ft/s, psf)
+  float kts_per_fps;
+  double cos_dE, sin_dE;     // rotation of the Earth per frame (omega * dt)
+  double dt;
+};
+
+static constexpr double WGS_A = 20925646.32546;
+static constexpr double WGS_B = 20855486.5951;
+static constexpr double GM_E = 14.0764417572e15;
+static constexpr double J2_E = 1.08262982e-03;
+static constexpr double OMEGA_E = 0.00007292115;
+static constexpr double E2 = 1.0 - (WGS_B * WGS_B) / (WGS_A * WGS_A);
+static constexpr double EC2 = 1.0 - E2;
+static constexpr double ELL_C = WGS_A * E2;
+static constexpr float S_W = 300.0f, B_W = 30.0f, CBAR = 11.32f;
+static constexpr float PI_F = 3.14159265358979323846f;
+static constexpr double PI_D = 3.14159265358979323846;
+static constexpr float RAD2DEG_F = 57.295779513082320876798f;
+
+// ------------------------------------------------------------------------------------------
+// lane state (registers) and its struct-of-arrays image in HBM
+// ------------------------------------------------------------------------------------------
+enum DField { D_RI0, D_RI1, D_RI2, D_VI0, D_VI1, D_VI2, D_EPA, D_EPRET, NDF };
+enum FField {
+  F_DV1 = 0,   // AB3 history as deltas: vI(k-1) - vI(k), vI(k-2) - vI(k)   (3+3)
+  F_DV2 = 3,
+  F_AI = 6,    // latest / previous inertial acceleration                   (3+3)
+  F_AIP = 9,
+  F_Q = 12,    // quaternion ECI->body                                      (4)
+  F_WI = 16,   // body rates wrt ECI                                        (3)
+  F_WID = 19,  // PQRidot                                                   (3)
+  F_BA = 22,   // body specific-force acceleration                          (3)
+  F_TEF = 25, F_AIL, F_ELE, F_RUD, F_LEF, F_SB,
+  F_PRI, F_PRP, F_PPI, F_PPP, F_PYI, F_PYP,
+  F_N1, F_N2,
+  F_LX,        // 10-entry auxiliary latch (F16L_*)
+  F_GOAL = F_LX + F16L_N,
+  F_LASTD = F_GOAL + 3,
+  F_WIND,
+  NFF = F_WIND + 3
+};
+enum IField { I_STEP, I_EPCOUNT, I_FLAGS, NIF };
+static constexpr int LANE_FLAG_AUG = 1;
+// persistent bytes per env (SURVEY.md 8d "S")
+static constexpr int STATE_BYTES = NDF * 8 + NFF * 4 + NIF * 4;
+
+struct SoA {
+  double* d;
+  float* f;
+  int32_t* i;
+  int64_t n;
+};
+
+struct Lane {
+  double rI[3], vI[3], epa, ep_ret;
+  float dv1[3], dv2[3], aI[3], aIp[3], q[4], wI[3], wId[3], ba[3];
+  float tef, ail, ele, rud, lef, sb;
+  float pri, prp, ppi, ppp, pyi, pyp;
+  float n1, n2;
+  float lx[F16L_N];
+  float goal[3], last_d, wind[3];
+  int32_t step, ep_count, flags;
+};
+
+__device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
+  const int64_t n = s.n;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    L.rI[j] = s.d[(D_RI0 + j) * n + k];
+    L.vI[j] = s.d[(D_VI0 + j) * n + k];
+  }
+  L.epa = s.d[D_EPA * n + k];
+  L.ep_ret = s.d[D_EPRET * n + k];
+  float* fl = reinterpret_cast<float*>(&L.dv1[0]);
+  (void)fl;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    L.dv1[j] = s.f[(F_DV1 + j) * n + k];
+    L.dv2[j] = s.f[(F_DV2 + j) * n + k];
+    L.aI[j] = s.f[(F_AI + j) * n + k];
+    L.aIp[j] = s.f[(F_AIP + j) * n + k];
+    L.wI[j] = s.f[(F_WI + j) * n + k];
+    L.wId[j] = s.f[(F_WID + j) * n + k];
+    L.ba[j] = s.f[(F_BA + j) * n + k];
+    L.goal[j] = s.f[(F_GOAL + j) * n + k];
+    L.wind[j] = s.f[(F_WIND + j) * n + k];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) L.q[j] = s.f[(F_Q + j) * n + k];
+  L.tef = s.f[F_TEF * n + k]; L.ail = s.f[F_AIL * n + k]; L.ele = s.f[F_ELE * n + k];
+  L.rud = s.f[F_RUD * n + k]; L.lef = s.f[F_LEF * n + k]; L.sb = s.f[F_SB * n + k];
+  L.pri = s.f[F_PRI * n + k]; L.prp = s.f[F_PRP * n + k];
+  L.ppi = s.f[F_PPI * n + k]; L.ppp = s.f[F_PPP * n + k];
+  L.pyi = s.f[F_PYI * n + k]; L.pyp = s.f[F_PYP * n + k];
+  L.n1 = s.f[F_N1 * n + k]; L.n2 = s.f[F_N2 * n + k];
+#pragma unroll
+  for (int j = 0; j < F16L_N; ++j) L.lx[j] = s.f[(F_LX + j) * n + k];
+  L.last_d = s.f[F_LASTD * n + k];
+  L.step = s.i[I_STEP * n + k];
+  L.ep_count = s.i[I_EPCOUNT * n + k];
+  L.flags = s.i[I_FLAGS * n + k];
+}
+
+__device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
+  const int64_t n = s.n;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    s.d[(D_RI0 + j) * n + k] = L.rI[j];
+    s.d[(D_VI0 + j) * n + k] = L.vI[j];
+  }
+  s.d[D_EPA * n + k] = L.epa;
+  s.d[D_EPRET * n + k] = L.ep_ret;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    s.f[(F_DV1 + j) * n + k] = L.dv1[j];
+    s.f[(F_DV2 + j) * n + k] = L.dv2[j];
+    s.f[(F_AI + j) * n + k] = L.aI[j];
+    s.f[(F_AIP + j) * n + k] = L.aIp[j];
+    s.f[(F_WI + j) * n + k] = L.wI[j];
+    s.f[(F_WID + j) * n + k] = L.wId[j];
+    s.f[(F_BA + j) * n + k] = L.ba[j];
+    s.f[(F_GOAL + j) * n + k] = L.goal[j];
+    s.f[(F_WIND + j) * n + k] = L.wind[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s.f[(F_Q + j) * n + k] = L.q[j];
+  s.f[F_TEF * n + k] = L.tef; s.f[F_AIL * n + k] = L.ail; s.f[F_ELE * n + k] = L.ele;
+  s.f[F_RUD * n + k] = L.rud; s.f[F_LEF * n + k] = L.lef; s.f[F_SB * n + k] = L.sb;
+  s.f[F_PRI * n + k] = L.pri; s.f[F_PRP * n + k] = L.prp;
+  s.f[F_PPI * n + k] = L.ppi; s.f[F_PPP * n + k] = L.ppp;
+  s.f[F_PYI * n + k] = L.pyi; s.f[F_PYP * n + k] = L.pyp;
+  s.f[F_N1 * n + k] = L.n1; s.f[F_N2 * n + k] = L.n2;
+#pragma unroll
+  for (int j = 0; j < F16L_N; ++j) s.f[(F_LX + j) * n + k] = L.lx[j];
+  s.f[F_LASTD * n + k] = L.last_d;
+  s.i[I_STEP * n + k] = L.step;
+  s.i[I_EPCOUNT * n + k] = L.ep_count;
+  s.i[I_FLAGS * n + k] = L.flags;
+}
+
+// ------------------------------------------------------------------------------------------
+// table lookups (FGTable semantics: clamped, no extrapolation). Breakpoints are literals.
+// ------------------------------------------------------------------------------------------
+struct Seg {  // bracketing segment i-1..i and clamped factor
+  int i;
+  float f;
+};
+// 2-D style bracket (FGTable::GetValue(row, col)): i in [1, n-1], factor clamped to [0,1].
+template <int N>
+__device__ __forceinline__ Seg bracket(const float (&bp)[N], float x) {
+  int i = 1;
+#pragma unroll
+  for (int k = 1; k < N - 1; ++k) i += (bp[k] < x) ? 1 : 0;
+  float lo = bp[0], hi = bp[1];
+#pragma unroll
+  for (int k = 2; k < N; ++k) {
+    lo = (i == k) ? bp[k - 1] : lo;
+    hi = (i == k) ? bp[k] : hi;
+  }
+  float f = (x - lo) / (hi - lo);
+  f = fminf(fmaxf(f, 0.0f), 1.0f);
+  return {i, f};
+}
+__device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (b - a) + a; }
+
+// 1-D lookup over an LDS value array with literal breakpoints (FGTable::GetValue(key))
+template <int N>
+__device__ __forceinline__ float tab1(const float (&bp)[N], const float* v, float x) {
+  if (x <= bp[0]) return v[0];
+  if (x >= bp[N - 1]) return v[N - 1];
+  Seg s = bracket(bp, x);
+  return lerp1(s.f, v[s.i - 1], v[s.i]);
+}
+// 2-D lookup, row-major [nr][nc] LDS values
+template <int NR, int NC>
+__device__ __forceinline__ float tab2(const float (&rb)[NR], const float (&cb)[NC], const float* v,
+                                      float x, float y) {
+  Seg r = bracket(rb, x), c = bracket(cb, y);
+  float a0 = v[(r.i - 1) * NC + c.i - 1], a1 = v[r.i * NC + c.i - 1];
+  float b0 = v[(r.i - 1) * NC + c.i], b1 = v[r.i * NC + c.i];
+  float c1 = lerp1(r.f, a0, a1);
+  float c2 = lerp1(r.f, b0, b1);
+  return c1 + c.f * (c2 - c1);
+}
+
+// ------------------------------------------------------------------------------------------
+// atmosphere: US-1976 (FGStandardAtmosphere), troposphere..mesosphere, English units out
+// ------------------------------------------------------------------------------------------
+struct Atm {
+  float T, P, rho, a;
+};
+__device__ __forceinline__ Atm atmosphere(float h_ft) {
+  // layer bases (geopotential m), lapse (K/m), base T (K), base P (Pa) -- same recurrence
+  // as the oracle, evaluated at compile time below
+  constexpr float Hb[8] = {0.0f, 11000.0f, 20000.0f, 32000.0f, 47000.0f, 51000.0f, 71000.0f, 84852.0f};
+  constexpr float Lb[7] = {-0.0065f, 0.0f, 0.001f, 0.0028f, 0.0f, -0.0028f, -0.002f};
+  constexpr float Tb[7] = {288.15f, 216.65f, 216.65f, 228.65f, 270.65f, 270.65f, 214.65f};
+  constexpr float Pb[7] = {101325.0f, 22632.064f, 5474.88867f, 868.018685f, 110.906306f,
+                           66.9388731f, 3.95642043f};  // oracle recurrence, rounded
+  constexpr float GMR = 9.80665f * 0.0289644f / 8.31432f;
+  constexpr float R = 8.31432f / 0.0289644f;
+  const float z = h_ft * 0.3048f;
+  const float H = 6356766.0f * z / (6356766.0f + z);
+  int b = 0;
+#pragma unroll
+  for (int k = 1; k < 7; ++k) b += (H >= Hb[k]) ? 1 : 0;
+  float hb = Hb[0], lb = Lb[0], tb = Tb[0], pb = Pb[0];
+#pragma unroll
+  for (int k = 1; k < 7; ++k) {
+    if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; }
+  }
+  float T, P;
+  if (lb != 0.0f) {
+    T = tb + lb * (H - hb);
+    P = pb * __powf(tb / T, GMR / lb);
+  } else {
+    T = tb;
+    P = pb * __expf(-GMR * (H - hb) / tb);
+  }
+  const float rho = P / (R * T);
+  Atm o;
+  o.T = T * 1.8f;
+  o.P = P * (1.0f / 47.88025898033584f);
+  o.rho = rho * (1.0f / 515.3788183931961f);
+  o.a = sqrtf(1.4f * R * T) * (1.0f / 0.3048f);
+  return o;
+}
+
+// FGAuxiliary::VcalibratedFromMach (kts)
+__device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts& C) {
+  if (!(fabsf(mach) > 0.0f)) return 0.0f;
+  float pt;
+  if (mach < 1.0f) {
+    float x = 1.0f + 0.2f * mach * mach;
+    pt = p * (x * x * x * sqrtf(x));
+  } else {
+    float m2 = mach * mach, d = 7.0f * m2 - 1.0f;
+    pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) / (d * d * sqrtf(d));
+  }
+  const float qc = pt - p;
+  const float A = qc / C.p_sl + 1.0f;
+  float M = sqrtf(5.0f * (__powf(A, 1.0f / 3.5f) - 1.0f));
+  if (M > 1.0f) {
+    for (int i = 0; i < 10; ++i) {
+      float t = 1.0f - 1.0f / (7.0f * M * M);
+      M = 0.8812848543473311f * sqrtf(A * (t * t * sqrtf(t)));
+    }
+  }
+  return C.a_sl * M * C.kts_per_fps;
+}
+
+// ------------------------------------------------------------------------------------------
+// frames
+// ------------------------------------------------------------------------------------------
+struct Derived {
+  float Ti2b[9], Tec2b[9], Tl2b[9];
+  float uvw[3], pqr[3], vned[3];
+  float gE[3];      // J2 gravity, ECEF
+  double h_ft;
+};
+
+__device__ __forceinline__ void quat_T(const float* q, float* T) {
+  const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const float q0q0 = q0 * q0, q1q1 = q1 * q1, q2q2 = q2 * q2, q3q3 = q3 * q3;
+  T[0] = q0q0 + q1q1 - q2q2 - q3q3;
+  T[1] = 2.0f * (q1 * q2 + q0 * q3);
+  T[2] = 2.0f * (q1 * q3 - q0 * q2);
+  T[3] = 2.0f * (q1 * q2 - q0 * q3);
+  T[4] = q0q0 - q1q1 + q2q2 - q3q3;
+  T[5] = 2.0f * (q2 * q3 + q0 * q1);
+  T[6] = 2.0f * (q1 * q3 + q0 * q2);
+  T[7] = 2.0f * (q2 * q3 - q0 * q1);
+  T[8] = q0q0 - q1q1 - q2q2 + q3q3;
+}
+__device__ __forceinline__ void mmul(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+__device__ __forceinline__ void mvec(const float* M, const float* v, float* o) {
+  o[0] = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  o[1] = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  o[2] = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+}
+__device__ __forceinline__ void mtvec(const float* M, const float* v, float* o) {
+  o[0] = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  o[1] = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  o[2] = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+}
+__device__ __forceinline__ void crossf(const float* a, const float* b, float* o) {
+  const float x = a[1] * b[2] - a[2] * b[1];
+  const float y = a[2] * b[0] - a[0] * b[2];
+  const float z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+// geodetic altitude from ECEF (Fukushima 2006, one Halley step; FGLocation), fp64
+__device__ __forceinline__ double geodetic_altitude(double x, double y, double z, double rxy) {
+  const double ec = WGS_B / WGS_A;
+  const double s0 = fabs(z);
+  const double zc = ec * s0, c0 = ec * rxy;
+  const double c02 = c0 * c0, s02 = s0 * s0;
+  const double a02 = c02 + s02, a0 = sqrt(a02), a03 = a02 * a0;
+  double s1 = zc * a03 + ELL_C * s02 * s0;
+  const double c1 = rxy * a03 - ELL_C * c02 * c0;
+  const double cs0c0 = ELL_C * c0 * s0;
+  const double b0 = 1.5 * cs0c0 * ((rxy * s0 - zc * c0) * a0 - cs0c0);
+  s1 = s1 * a03 - b0 * s0;
+  const double cc = ec * (c1 * a03 - b0 * c0);
+  const double s12 = s1 * s1, cc2 = cc * cc;
+  const double norm = sqrt(s12 + cc2);
+  return (rxy * cc + s0 * s1 - WGS_A * sqrt(EC2 * s12 + cc2)) / norm;
+  (void)x; (void)y;
+}
+
+// Everything FGPropagate / FGInertial derive from the integrated state.
+// ce, se: cos/sin of the Earth position angle (fp64).
+__device__ __forceinline__ void derive(const Lane& L, double ce, double se, Derived& d,
+                                       float* lat_gc_out = nullptr, float* lon_out = nullptr) {
+  const double xE = ce * L.rI[0] + se * L.rI[1];
+  const double yE = -se * L.rI[0] + ce * L.rI[1];
+  const double zE = L.rI[2];
+  const double rxy = sqrt(xE * xE + yE * yE);
+  const double r = sqrt(rxy * rxy + zE * zE);
+  const double inv_r = 1.0 / r;
+  const float slat = (float)(zE * inv_r), clat = (float)(rxy * inv_r);
+  float slon = 0.0f, clon = 1.0f;
+  if (rxy != 0.0) {
+    const double inv = 1.0 / rxy;
+    slon = (float)(yE * inv);
+    clon = (float)(xE * inv);
+  }
+  d.h_ft = geodetic_altitude(xE, yE, zE, rxy);
+  if (lat_gc_out) {
+    *lat_gc_out = (float)atan2(zE, rxy);
+    *lon_out = (rxy == 0.0) ? 0.0f : (float)atan2(yE, xE);
+  }
+  // Tec2l (geocentric, FGLocation)
+  const float L0 = -clon * slat, L1 = -slon * slat, L2 = clat;
+  const float L3 = -slon, L4 = clon;
+  const float L6 = -clon * clat, L7 = -slon * clat, L8 = -slat;
+  quat_T(L.q, d.Ti2b);
+  const float c = (float)ce, s = (float)se;
+  // Tec2b = Ti2b * Tec2i, Tec2i = [c -s 0; s c 0; 0 0 1]
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float a = d.Ti2b[3 * i], b = d.Ti2b[3 * i + 1];
+    d.Tec2b[3 * i] = a * c + b * s;
+    d.Tec2b[3 * i + 1] = -a * s + b * c;
+    d.Tec2b[3 * i + 2] = d.Ti2b[3 * i + 2];
+  }
+  // Tl2b = Tec2b * Tl2ec (Tl2ec = Tec2l^T)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float a = d.Tec2b[3 * i], b = d.Tec2b[3 * i + 1], e = d.Tec2b[3 * i + 2];
+    d.Tl2b[3 * i] = a * L0 + b * L1 + e * L2;
+    d.Tl2b[3 * i + 1] = a * L3 + b * L4;
+    d.Tl2b[3 * i + 2] = a * L6 + b * L7 + e * L8;
+  }
+  // vUVW = Ti2b * (vI - w x rI)
+  const float vr[3] = {(float)(L.vI[0] + OMEGA_E * L.rI[1]), (float)(L.vI[1] - OMEGA_E * L.rI[0]),
+                       (float)L.vI[2]};
+  mvec(d.Ti2b, vr, d.uvw);
+  // vPQR = vPQRi - Ti2b * (0,0,w)
+  const float we = (float)OMEGA_E;
+  d.pqr[0] = L.wI[0] - d.Ti2b[2] * we;
+  d.pqr[1] = L.wI[1] - d.Ti2b[5] * we;
+  d.pqr[2] = L.wI[2] - d.Ti2b[8] * we;
+  mtvec(d.Tl2b, d.uvw, d.vned);
+  // J2 gravity (FGInertial::GetGravityJ2), ECEF
+  const float rf = (float)r;
+  const float adivr = (float)(WGS_A * inv_r);
+  const float pre = 1.5f * (float)J2_E * adivr * adivr;
+  const float gm = (float)(GM_E * inv_r * inv_r);
+  const float xy = 1.0f - 5.0f * slat * slat, zz = 3.0f - 5.0f * slat * slat;
+  const float kxy = -gm * (1.0f + pre * xy);
+  d.gE[0] = kxy * (float)(xE * inv_r);
+  d.gE[1] = kxy * (float)(yE * inv_r);
+  d.gE[2] = -gm * (1.0f + pre * zz) * slat;
+  (void)rf;
+}
+
+// Euler angles from Tl2b (FGMatrix33::GetEuler)
+__device__ __forceinline__ void euler(const float* T, float& phi, float& tht, float& psi) {
+  if (T[2] <= -1.0f) {
+    tht = 0.5f * PI_F; phi = atan2f(-T[7], T[4]); psi = 0.0f;
+  } else if (T[2] >= 1.0f) {
+    tht = -0.5f * PI_F; phi = atan2f(-T[7], T[4]); psi = 0.0f;
+  } else {
+    tht = asinf(-T[2]);
+    phi = atan2f(T[5], T[8]);
+    float p = atan2f(T[1], T[0]);
+    if (p < 0.0f) p += 2.0f * PI_F;
+    psi = p;
+  }
+}
+
+// FCS components
+__device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ bool eq_roundoff(float a, float b) {
+  return fabsf(a - b) <= 2.0f * 1.1920929e-07f * fmaxf(fabsf(a), fabsf(b));
+}
+// FGKinematic with two detents (single segment): rate = (d1 - d0) / t
+__device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float rate, float dt,
+                                      bool ic) {
+  in = clipf(in, d0, d1);
+  if (ic) return in;
+  if (eq_roundoff(in, out)) return out;
+  const float tdt = fabsf((in - out) / rate);
+  if (dt < tdt) return (out < in) ? out + dt * rate : out - dt * rate;
+  return in;
+}
+// TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350)
+__device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic) {
+  in = clipf(in, -1.0f, 1.0f);
+  if (ic) return in;
+  float dt0 = dt;
+  for (int g = 0; g < 8 && dt0 > 0.0f && !eq_roundoff(in, out); ++g) {
+    // segment search (direction dependent), n = 3
+    const int ind = (in < out) ? ((0.0f < out) ? 2 : 1) : ((0.0f <= out) ? 2 : 1);
+    if (ind == 1) { out = in; break; }  // transition time 0 -> infinite rate
+    const float rate = 1.0f / 3.0f, lo = 0.0f, hi = 1.0f;
+    const float tin = clipf(in, lo, hi);
+    float tdt = fabsf((tin - out) / rate);
+    if (dt0 < tdt) {
+      tdt = dt0;
+      out = (out < in) ? out + tdt * rate : out - tdt * rate;
+    } else {
+      out = tin;
+    }
+    dt0 -= tdt;
+  }
+  return out;
+}
+__device__ __forceinline__ float pidf(float in, float& itot, float& prev, float trig, float kp,
+                                      float ki, float kd, float dt, bool ic) {
+  const float dval = ic ? 0.0f : (in - prev) / dt;
+  const float delta = (!ic && fabsf(trig) < 0.000001f) ? in : 0.0f;
+  if (trig < 0.0f) itot = 0.0f;
+  itot += ki * dt * delta;
+  const float out = kp * in + itot + kd * dval;
+  prev = in;
+  return out;
+}
+__device__ __forceinline__ float aero_scale(float in, float outmax) {
+  // zero-centred aerosurface_scale with symmetric domain [-1,1] and range [-outmax,outmax]
+  return (in == 0.0f) ? 0.0f : in * outmax;
+}
+
+struct FcsOut {
+  float de, da, dr, dlef, flap_mix, dsb, throttle;
+};
+
+// f16.xml:309-984 (document order). T = LDS table blob.
+__device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33, float v_fps,
+                                        const float* T, float dt, bool ic, FcsOut& o) {
+  const float alpha = L.lx[F16L_ALPHA], mach = L.lx[F16L_MACH], vc = L.lx[F16L_VC_KTS];
+  const float vg = L.lx[F16L_VG_FPS];
+  // Flaps
+  float tef_rad = 0.0f;
+  if (vc < 250.0f) tef_rad = 0.349f;
+  else if (mach > 0.9f) tef_rad = -0.0349f;
+  L.tef = kin_tef(L.tef, tef_rad * 2.864789f, dt, ic);
+  // Roll
+  const float roll_err = cmd[0] - L.lx[F16L_P_AERO] * 0.31821f;
+  const float ail_trig = (vc < 20.0f) ? 0.0f : 1.0f;
+  const float roll_pid = pidf(roll_err, L.pri, L.prp, ail_trig, 3.0f, 0.0005f, -0.00125f, dt, ic);
+  const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
+  o.da = aero_scale(roll_cmd, 0.375f);
+  L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
+  const float asc = L.ail * tab1(BP_fcs_aileron_speed_compensated,
+                                 T + OFF_fcs_v_aileron_speed_compensated, mach);
+  const float lflap = clipf(-L.tef - asc, -1.0f, 1.0f);
+  const float rflap = clipf(L.tef - asc, -1.0f, 1.0f);
+  o.flap_mix = (lflap + rflap) * 1.4324f;
+  // Pitch
+  const float g_corr = L.lx[F16L_NPZ] - tl2b_33;  // cos(theta)cos(phi) == Tl2b(3,3)
+  const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
+  const float ele_sched = ele_lim * tab1(BP_fcs_elevator_scheduler, T + OFF_fcs_v_elevator_scheduler, alpha);
+  const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
+  const float ele_trig = (vc < 5.0f) ? 0.0f : 1.0f;
+  const float gpid = clipf(pidf(pitch_err, L.ppi, L.ppp, ele_trig, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
+  const float pitch_sched = clipf(ele_sched + alpha * 1.0472f + gpid, -1.0f, 1.0f);
+  L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
+  o.de = aero_scale(L.ele, 0.436f);
+  // Yaw
+  const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tab1(BP_fcs_yaw_rate_norm, T + OFF_fcs_v_yaw_rate_norm, vg) +
+                        L.lx[F16L_NPY] * 0.25f;
+  const float rud_trig = (vc < 10.0f) ? 0.0f : 1.0f;
+  const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, rud_trig, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
+  const float yaw_sched = clipf(cmd[2] + ypid, -1.0f, 1.0f);
+  L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, 2.0f / 0.4f, dt, ic);
+  o.dr = aero_scale(L.rud, 0.524f);
+  // Leading edge flap (gear pinned up, no WOW)
+  float lef_rad = 0.0f;
+  if (alpha > 0.2618f) lef_rad = 0.436f;
+  else if (alpha > 0.0873f) lef_rad = 0.262f;
+  else if (mach > 0.9f) lef_rad = -0.0349f;
+  o.dlef = lef_rad;
+  L.lef = kin2(L.lef, lef_rad * 2.293578f, -1.0f, 1.0f, 2.0f / 3.0f, dt, ic);
+  // Throttle
+  o.throttle = cmd[3] * 2.0f;
+  // Speedbrake
+  const float sb_init = (alpha * RAD2DEG_F >= 53.0f && v_fps <= 18.0f) ? 1.0f : 0.0f;
+  const float sb_sched = sb_init * T[OFF_fcs_v_speedbrake_scheduler];  // gear-cmd-norm = 0
+  L.sb = kin2(L.sb, sb_sched * 60.0f, 0.0f, 60.0f, 60.0f, dt, ic);
+  o.dsb = L.sb * (1.0f / RAD2DEG_F);
+}
+
+// FGTurbine tpRun, augmethod 2
+__device__ __forceinline__ float seekf(float v, float target, float accel, float decel, float dt) {
+  if (v > target) {
+    v -= dt * decel;
+    if (v < target) v = target;
+  } else if (v < target) {
+    v += dt * accel;
+    if (v > target) v = target;
+  }
+  return v;
+}
+__device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float mach, float h_rho,
+                                            float sigma, const float* T, float dt, bool ic) {
+  float tp = throttle_pos, aug_cmd = 0.0f;
+  if (tp > 1.0f) { aug_cmd = tp - 1.0f; tp -= aug_cmd; }
+  const float idle = 17800.0f * tab2(BP_engr_IdleThrust, BP_engc_IdleThrust, T + OFF_eng_v_IdleThrust, mach, h_rho);
+  const float mil = (17800.0f - idle) * tab2(BP_engr_MilThrust, BP_engc_MilThrust, T + OFF_eng_v_MilThrust, mach, h_rho);
+  if (ic) {
+    L.n2 = 60.0f + tp * 40.0f;
+    L.n1 = 30.0f + tp * 70.0f;
+    L.flags = (aug_cmd > 0.0f) ? (L.flags | LANE_FLAG_AUG) : (L.flags & ~LANE_FLAG_AUG);
+  } else {
+    const float nn = fminf((L.n2 - 60.0f) * (1.0f / 40.0f) + 0.1f, 1.0f);
+    const float u = 1.0f - nn;
+    const float spool = (90.0f / 3.36f) / (1.0f + 3.0f * u * u * u + (1.0f - sigma));
+    L.n2 = seekf(L.n2, 60.0f + tp * 40.0f, spool, spool * 3.0f, dt);
+    L.n1 = seekf(L.n1, 30.0f + tp * 70.0f, spool, spool * 2.4f, dt);
+  }
+  const float n2n = (L.n2 - 60.0f) * (1.0f / 40.0f);
+  float thrust = idle + mil * n2n * n2n;
+  if (!(L.flags & LANE_FLAG_AUG)) thrust *= (1.0f - 0.03f);
+  if (aug_cmd > 0.0f) {
+    L.flags |= LANE_FLAG_AUG;
+    const float tdiff = 29000.0f * tab2(BP_engr_AugThrust, BP_engc_AugThrust, T + OFF_eng_v_AugThrust, mach, h_rho) - thrust;
+    thrust += tdiff * aug_cmd;
+  } else {
+    L.flags &= ~LANE_FLAG_AUG;
+  }
+  return thrust;
+}
+
+// Aerodynamics (f16.xml:986-1917), hand-fused: shared (index, factor) per breakpoint vector.
+struct AeroIn {
+  float qbar, alpha, beta, mach, p, q, r, bi2vel, ci2vel, kclge;
+  float de, da, dr, dlef, flap, dsb;
+};
+__device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6) {
+  const Seg sa = bracket(BP_alpha_bp, a.alpha);
+  // 16 alpha 1-D tables, [12][16] interleaved; FGTable 1-D semantics (clamp at the ends)
+  float A[F16_N_A1D];
+  {
+    const float* r0 = T + OFF_alpha1d + (sa.i - 1) * F16_N_A1D;
+    const float* r1 = r0 + F16_N_A1D;
+    const bool lo = a.alpha <= BP_alpha_bp[0], hi = a.alpha >= BP_alpha_bp[F16_N_ALPHA - 1];
+#pragma unroll
+    for (int k = 0; k < F16_N_A1D; ++k) {
+      float v = lerp1(sa.f, r0[k], r1[k]);
+      v = lo ? r0[k] : v;
+      v = hi ? r1[k] : v;
+      A[k] = v;
+    }
+  }
+  // 2-D alpha x elevator: CDDh, CLDh, CmDh ([12][5][3])
+  const Seg se = bracket(BP_de_bp, a.de);
+  float ADE[3];
+  {
+    const float* p00 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 3;
+    const float* p10 = p00 + F16_N_DE * 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c1 = lerp1(sa.f, p00[k], p10[k]);
+      const float c2 = lerp1(sa.f, p00[k + 3], p10[k + 3]);
+      ADE[k] = c1 + se.f * (c2 - c1);
+    }
+  }
+  const Seg sb13 = bracket(BP_beta13_bp, a.beta);
+  float AB13[2];
+  {
+    const float* p00 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 2;
+    const float* p10 = p00 + F16_N_B13 * 2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float c1 = lerp1(sa.f, p00[k], p10[k]);
+      const float c2 = lerp1(sa.f, p00[k + 2], p10[k + 2]);
+      AB13[k] = c1 + sb13.f * (c2 - c1);
+    }
+  }
+  const Seg sb7 = bracket(BP_beta7_bp, a.beta);
+  float AB7[4];
+  {
+    const float* p00 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 4;
+    const float* p10 = p00 + F16_N_B7 * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float c1 = lerp1(sa.f, p00[k], p10[k]);
+      const float c2 = lerp1(sa.f, p00[k + 4], p10[k + 4]);
+      AB7[k] = c1 + sb7.f * (c2 - c1);
+    }
+  }
+  const float m = a.mach;
+  const float CDmach = tab1(BP_mach_CDmach, T + OFF_mach_v_CDmach, m);
+  const float CYb_M = tab1(BP_mach_CYb_M, T + OFF_mach_v_CYb_M, m);
+  const float Clb_M = tab1(BP_mach_Clb_M, T + OFF_mach_v_Clb_M, m);
+  const float Clda_M = tab1(BP_mach_Clda_M, T + OFF_mach_v_Clda_M, m);
+  const float Cldr_M = tab1(BP_mach_Cldr_M, T + OFF_mach_v_Cldr_M, m);
+  const float Cma_M = tab1(BP_mach_Cma_M, T + OFF_mach_v_Cma_M, m);
+  const float Cnb_M = tab1(BP_mach_Cnb_M, T + OFF_mach_v_Cnb_M, m);
+  const float Cnda_M = tab1(BP_mach_Cnda_M, T + OFF_mach_v_Cnda_M, m);
+  const float Cndr_M = tab1(BP_mach_Cndr_M, T + OFF_mach_v_Cndr_M, m);
+
+  const float qS = a.qbar * S_W;
+  const float qc = a.q * a.ci2vel, pb = a.p * a.bi2vel, rb = a.r * a.bi2vel;
+  // DRAG (f16.xml:1010-1174)
+  const float D = qS * (ADE[ADE_CDDh] + CDmach + a.dlef * A[A1D_CDDlef] + a.flap * 0.08f +
+                        0.0f * 0.027f + a.dsb * A[A1D_CDDsb] + qc * A[A1D_CDq] +
+                        qc * a.dlef * A[A1D_CDq_Dlef]);
+  // SIDE (:1176-1272)
+  const float Y = qS * (a.beta * -1.146f + a.beta * CYb_M + a.da * -0.0226f + a.dr * 0.086f +
+                        pb * A[A1D_CYp] + rb * A[A1D_CYr]);
+  // LIFT (:1274-1418)
+  const float Lf = qS * (a.kclge * ADE[ADE_CLDh] + a.dlef * a.kclge * A[A1D_CLDlef] +
+                         a.flap * a.kclge * 0.35f + a.kclge * a.dsb * A[A1D_CLDsb] +
+                         qc * a.kclge * A[A1D_CLq] + qc * a.dsb * A[A1D_CLq_Dsb]);
+  const float qSb = qS * B_W, qSc = qS * CBAR;
+  // ROLL (:1420-1613)
+  const float Lm = qSb * (AB13[AB13_Clb] + a.beta * Clb_M + pb * A[A1D_Clp] + rb * A[A1D_Clr] +
+                          a.da * AB7[AB7_Clda] + a.alpha * a.da * Clda_M + a.alpha * a.dr * Cldr_M +
+                          a.dr * AB7[AB7_Cldr]);
+  // PITCH (:1615-1716)
+  const float Mm = qSc * (ADE[ADE_CmDh] + a.alpha * Cma_M + a.dsb * A[A1D_CmDsb] + qc * A[A1D_Cmq]);
+  // YAW (:1718-1916)
+  const float Nm = qSb * (AB13[AB13_Cnb] + a.beta * Cnb_M + pb * A[A1D_Cnp] + rb * A[A1D_Cnr] +
+                          a.da * Cnda_M + a.da * AB7[AB7_Cnda] + a.dr * AB7[AB7_Cndr] +
+                          a.alpha * a.dr * Cndr_M);
+  F6[0] = D; F6[1] = Y; F6[2] = Lf; F6[3] = Lm; F6[4] = Mm; F6[5] = Nm;
+}
+
+// One FGFDMExec::Run(). ce/se: Earth angle cos/sin at the START of the frame (updated here).
+__device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se,
+                                      const float* T, const ModelConsts& C, bool ic) {
+  const float dt = (float)C.dt;
+  if (!ic) {
+    // -- FGPropagate: integrate with the previous frame's derivatives --
+    const float hx = 0.5f * dt * L.wI[0], hy = 0.5f * dt * L.wI[1], hz = 0.5f * dt * L.wI[2];
+    const float a2 = hx * hx + hy * hy + hz * hz;
+    float ca, sa;
+    if (a2 < 1e-2f) {  // |angle| < 0.1: series (error < 1e-11)
+      ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f)));
+      sa = 1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f)));
+    } else {
+      const float ang = sqrtf(a2);
+      ca = cosf(ang);
+      sa = sinf(ang) / ang;
+    }
+    const float p0 = ca, p1 = hx * sa, p2 = hy * sa, p3 = hz * sa;
+    const float q0 = L.q[0], q1 = L.q[1], q2 = L.q[2], q3 = L.q[3];
+    float n0 = q0 * p0 - q1 * p1 - q2 * p2 - q3 * p3;
+    float n1 = q0 * p1 + q1 * p0 + q2 * p3 - q3 * p2;
+    float n2 = q0 * p2 - q1 * p3 + q2 * p0 + q3 * p1;
+    float n3 = q0 * p3 + q1 * p2 - q2 * p1 + q3 * p0;
+    const float rn = rsqrtf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+    L.q[0] = n0 * rn; L.q[1] = n1 * rn; L.q[2] = n2 * rn; L.q[3] = n3 * rn;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) L.wI[j] += dt * L.wId[j];
+    // AB3 position: r += dt/12 (23 v0 - 16 v1 + 5 v2) = dt v0 + dt/12 (-16 dv1 + 5 dv2)
+    // AB2 velocity: v += dt (1.5 a - 0.5 ap)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float corr = (dt * (1.0f / 12.0f)) * (-16.0f * L.dv1[j] + 5.0f * L.dv2[j]);
+      L.rI[j] += C.dt * L.vI[j] + (double)corr;
+      const float dv = dt * (1.5f * L.aI[j] - 0.5f * L.aIp[j]);
+      L.vI[j] += (double)dv;
+      L.dv2[j] = L.dv1[j] - dv;
+      L.dv1[j] = -dv;
+      L.aIp[j] = L.aI[j];
+    }
+    L.epa += OMEGA_E * C.dt;
+    const double c2 = ce * C.cos_dE - se * C.sin_dE;
+    const double s2 = se * C.cos_dE + ce * C.sin_dE;
+    ce = c2; se = s2;
+  }
+  Derived d;
+  derive(L, ce, se, d);
+  // -- Atmosphere (standard day: density altitude == altitude) --
+  const float h = (float)d.h_ft;
+  const Atm atm = atmosphere(h);
+  const float sigma = atm.rho / C.rho_sl;
+  // -- Systems --
+  FcsOut fc;
+  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, dt, ic, fc);
+  // -- Auxiliary --
+  float wb[3];
+  mvec(d.Tl2b, L.wind, wb);
+  const float ua = d.uvw[0] - wb[0], va = d.uvw[1] - wb[1], wa = d.uvw[2] - wb[2];
+  const float muw = ua * ua + wa * wa;
+  const float vt = sqrtf(muw + va * va);
+  const float alpha = muw > 0.0f ? atan2f(wa, ua) : 0.0f;
+  const float suw = sqrtf(muw);
+  const float beta = muw > 0.0f ? atan2f(va, suw) : 0.0f;
+  const float qbar = 0.5f * atm.rho * vt * vt;
+  const float mach = vt / atm.a;
+  const float vc = vcas_kts(mach, atm.P, C);
+  const float vg = sqrtf(d.vned[0] * d.vned[0] + d.vned[1] * d.vned[1]);
+  float bi2vel = 0.0f, ci2vel = 0.0f;
+  if (vt != 0.0f) {
+    const float inv2v = 0.5f / vt;
+    bi2vel = B_W * inv2v;
+    ci2vel = CBAR * inv2v;
+  }
+  float t1[3], t2[3], t3[3];
+  crossf(L.wId, C.eye, t1);
+  crossf(L.wI, C.eye, t2);
+  crossf(L.wI, t2, t3);
+  const float npy = (L.ba[1] + t1[1] + t3[1]) * C.inv_gref;
+  const float npz = (L.ba[2] + t1[2] + t3[2]) * C.inv_gref;
+  // h_b-mac = (h - (Tb2l * rp)_down) / b
+  const float vmac_d = d.Tl2b[2] * C.rp[0] + d.Tl2b[5] * C.rp[1] + d.Tl2b[8] * C.rp[2];
+  const float hbmac = (h - vmac_d) * (1.0f / B_W);
+  L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;
+  L.lx[F16L_VC_KTS] = vc; L.lx[F16L_VG_FPS] = vg;
+  L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
+  L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
+  // -- Propulsion --
+  const float thrust = engine_run(L, fc.throttle, mach, h, sigma, T, dt, ic);
+  // -- Aerodynamics --
+  AeroIn ai;
+  ai.qbar = qbar; ai.alpha = alpha; ai.beta = beta; ai.mach = mach;
+  ai.p = d.pqr[0]; ai.q = d.pqr[1]; ai.r = d.pqr[2];
+  ai.bi2vel = bi2vel; ai.ci2vel = ci2vel;
+  ai.kclge = tab1(BP_kclge, T + OFF_kclge_v, hbmac);
+  ai.de = fc.de; ai.da = fc.da; ai.dr = fc.dr; ai.dlef = fc.dlef; ai.flap = fc.flap_mix; ai.dsb = fc.dsb;
+  float A6[6];
+  aero(ai, T, A6);
+  // wind (D, Y, L) -> body, vFw = (-D, Y, -L)
+  float ca_ = 1.0f, sa_ = 0.0f, cb_ = 1.0f, sb_ = 0.0f;
+  if (muw > 0.0f) {
+    const float iuw = 1.0f / suw;
+    ca_ = ua * iuw; sa_ = wa * iuw;
+    const float ivt = 1.0f / vt;
+    cb_ = suw * ivt; sb_ = va * ivt;
+  }
+  const float fw0 = -A6[0], fw1 = A6[1], fw2 = -A6[2];
+  float F[3], M[3];
+  F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
+  F[1] = sb_ * fw0 + cb_ * fw1;
+  F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
+  float rxF[3];
+  crossf(C.rp, F, rxF);
+  M[0] = A6[3] + rxF[0];
+  M[1] = A6[4] + rxF[1];
+  M[2] = A6[5] + rxF[2];
+  // thrust along +x at the thruster: r x (T,0,0) = (0, rz T, -ry T)
+  F[0] += thrust;
+  M[1] += C.eng[2] * thrust;
+  M[2] += -C.eng[1] * thrust;
+  // -- Accelerations --
+#pragma unroll
+  for (int j = 0; j < 3; ++j) L.ba[j] = F[j] * C.inv_mass;
+  float gb[3];
+  mvec(d.Tec2b, d.gE, gb);
+  const float acc[3] = {L.ba[0] + gb[0], L.ba[1] + gb[1], L.ba[2] + gb[2]};
+  mtvec(d.Ti2b, acc, L.aI);
+  float Jw[3], wxJw[3], rhs[3];
+  mvec(C.J, L.wI, Jw);
+  crossf(L.wI, Jw, wxJw);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) rhs[j] = M[j] - wxJw[j];
+  mvec(C.Jinv, rhs, L.wId);
+}
+
+}  // namespace f16

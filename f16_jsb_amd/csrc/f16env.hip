@@ -1,0 +1,765 @@
+// f16env.hip -- HIP kernels (gfx950) + the extern "C" ABI declared in include/f16env.h.
+//
+// Hot path: k_step = one VecEnv step for N envs in ONE launch: 4 FDM frames per lane with
+// the state in VGPRs (f16_device.h), then the env layer of jsbsim_gym/jsbsim_gym.py
+// (:172-197 frame, :237-261 reward/termination, :487-509 shaping, TimeLimit, Monitor
+// stats) and the DummyVecEnv auto-reset (dummy_vec_env.py:56-73) for lanes that finished,
+// with the ordered K-frame stack rebuilt by a coalesced per-wave row copy.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/f16env.h"
+#include "f16_device.h"
+
+using namespace f16;
+
+// ------------------------------------------------------------------------------------------
+// error handling
+// ------------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int set_err(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      char b_[256];                                                                 \
+      snprintf(b_, sizeof b_, "%s failed: %s", #x, hipGetErrorString(e_));          \
+      return set_err(-2, b_);                                                       \
+    }                                                                               \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 (same stream definition as oracle/f16ref.c)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
+                                       uint32_t c2, uint32_t c3, uint32_t* o) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
+}
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+// goal RNG: jsbsim_gym.py:312-323 formula on a Philox stream keyed by (seed; gid, episode)
+__device__ __forceinline__ void rng_goal(uint64_t seed, uint64_t gid, uint32_t ep, float* g) {
+  uint32_t o[4], o2[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), ep,
+         0x474F414Cu, o);
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), ep,
+         0x474F414Cu ^ 1u, o2);
+  const double dist = 1000.0 + (10000.0 - 1000.0) * u53(o[0], o[1]);
+  const double bear = 0.0 + (2.0 * PI_D - 0.0) * u53(o[2], o[3]);
+  const double alt = 1000.0 + (4000.0 - 1000.0) * u53(o2[0], o2[1]);
+  g[0] = (float)(dist * cos(bear));
+  g[1] = (float)(dist * sin(bear));
+  g[2] = (float)alt;
+}
+
+// ------------------------------------------------------------------------------------------
+// IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
+// ------------------------------------------------------------------------------------------
+__device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelConsts& C) {
+  const double lat = ic[F16_IC_LAT_GEOD_RAD], lon = ic[F16_IC_LON_RAD], h = ic[F16_IC_H_SL_FT];
+  const double sl = sin(lat), cl = cos(lat);
+  const double N = WGS_A / sqrt(1.0 - E2 * sl * sl);
+  const double rE[3] = {(N + h) * cl * cos(lon), (N + h) * cl * sin(lon), (EC2 * N + h) * sl};
+  L.epa = 0.0;
+  for (int j = 0; j < 3; ++j) L.rI[j] = rE[j];
+  const double rxy = sqrt(rE[0] * rE[0] + rE[1] * rE[1]);
+  const double r = sqrt(rxy * rxy + rE[2] * rE[2]);
+  const double slat = rE[2] / r, clat = rxy / r;
+  const double slon = rxy == 0.0 ? 0.0 : rE[1] / rxy, clon = rxy == 0.0 ? 1.0 : rE[0] / rxy;
+  const double Lm[9] = {-clon * slat, -slon * slat, clat, -slon, clon, 0.0, -clon * clat, -slon * clat, -slat};
+  const double ph = ic[F16_IC_PHI_RAD], th = ic[F16_IC_THETA_RAD], ps = ic[F16_IC_PSI_RAD];
+  const double cp = cos(ph), sp = sin(ph), ct = cos(th), st = sin(th), cs = cos(ps), ss = sin(ps);
+  const double Tl[9] = {ct * cs, ct * ss, -st,
+                        sp * st * cs - cp * ss, sp * st * ss + cp * cs, sp * ct,
+                        cp * st * cs + sp * ss, cp * st * ss - sp * cs, cp * ct};
+  double Ti[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ti[3 * i + j] = Tl[3 * i] * Lm[j] + Tl[3 * i + 1] * Lm[3 + j] + Tl[3 * i + 2] * Lm[6 + j];
+  // FGMatrix33::GetQuaternion
+  double t[4] = {1.0 + Ti[0] + Ti[4] + Ti[8], 1.0 + Ti[0] - Ti[4] - Ti[8],
+                 1.0 - Ti[0] + Ti[4] - Ti[8], 1.0 - Ti[0] - Ti[4] + Ti[8]};
+  int idx = 0;
+  for (int i = 1; i < 4; ++i)
+    if (t[i] > t[idx]) idx = i;
+  double q[4];
+  if (idx == 0) {
+    q[0] = 0.5 * sqrt(t[0]);
+    q[1] = 0.25 * (Ti[5] - Ti[7]) / q[0]; q[2] = 0.25 * (Ti[6] - Ti[2]) / q[0]; q[3] = 0.25 * (Ti[1] - Ti[3]) / q[0];
+  } else if (idx == 1) {
+    q[1] = 0.5 * sqrt(t[1]);
+    q[0] = 0.25 * (Ti[5] - Ti[7]) / q[1]; q[2] = 0.25 * (Ti[1] + Ti[3]) / q[1]; q[3] = 0.25 * (Ti[2] + Ti[6]) / q[1];
+  } else if (idx == 2) {
+    q[2] = 0.5 * sqrt(t[2]);
+    q[0] = 0.25 * (Ti[6] - Ti[2]) / q[2]; q[1] = 0.25 * (Ti[1] + Ti[3]) / q[2]; q[3] = 0.25 * (Ti[5] + Ti[7]) / q[2];
+  } else {
+    q[3] = 0.5 * sqrt(t[3]);
+    q[0] = 0.25 * (Ti[1] - Ti[3]) / q[3]; q[1] = 0.25 * (Ti[2] + Ti[6]) / q[3]; q[2] = 0.25 * (Ti[5] + Ti[7]) / q[3];
+  }
+  if (q[0] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
+  const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  for (int i = 0; i < 4; ++i) { q[i] /= qn; L.q[i] = (float)q[i]; }
+  // Ti2b from the normalised quaternion (double), velocities
+  const double q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const double T0 = q0 * q0 + q1 * q1 - q2 * q2 - q3 * q3, T1 = 2.0 * (q1 * q2 + q0 * q3), T2 = 2.0 * (q1 * q3 - q0 * q2);
+  const double T3 = 2.0 * (q1 * q2 - q0 * q3), T4 = q0 * q0 - q1 * q1 + q2 * q2 - q3 * q3, T5 = 2.0 * (q2 * q3 + q0 * q1);
+  const double T6 = 2.0 * (q1 * q3 + q0 * q2), T7 = 2.0 * (q2 * q3 - q0 * q1), T8 = q0 * q0 - q1 * q1 - q2 * q2 + q3 * q3;
+  const double u = ic[F16_IC_U_FPS], v = ic[F16_IC_V_FPS], w = ic[F16_IC_W_FPS];
+  const double vb[3] = {T0 * u + T3 * v + T6 * w, T1 * u + T4 * v + T7 * w, T2 * u + T5 * v + T8 * w};
+  L.vI[0] = vb[0] - OMEGA_E * L.rI[1];
+  L.vI[1] = vb[1] + OMEGA_E * L.rI[0];
+  L.vI[2] = vb[2];
+  L.wI[0] = (float)(ic[F16_IC_P_RPS] + T2 * OMEGA_E);
+  L.wI[1] = (float)(ic[F16_IC_Q_RPS] + T5 * OMEGA_E);
+  L.wI[2] = (float)(ic[F16_IC_R_RPS] + T8 * OMEGA_E);
+  for (int j = 0; j < 3; ++j) {
+    L.wId[j] = 0.0f; L.ba[j] = 0.0f; L.aI[j] = 0.0f; L.aIp[j] = 0.0f; L.dv1[j] = 0.0f; L.dv2[j] = 0.0f;
+    L.wind[j] = (float)ic[F16_IC_WIND_N_FPS + j];
+  }
+  L.tef = L.ail = L.ele = L.rud = L.lef = L.sb = 0.0f;
+  L.pri = L.prp = L.ppi = L.ppp = L.pyi = L.pyp = 0.0f;
+  L.n1 = 30.0f; L.n2 = 60.0f; L.flags = 0;
+  for (int j = 0; j < F16L_N; ++j) L.lx[j] = 0.0f;
+  const float cmd[4] = {(float)ic[F16_IC_CMD_AIL], (float)ic[F16_IC_CMD_ELE], (float)ic[F16_IC_CMD_RUD],
+                        (float)ic[F16_IC_CMD_THR]};
+  double ce = 1.0, se = 0.0;
+  frame(L, cmd, ce, se, T, C, true);
+  frame(L, cmd, ce, se, T, C, true);
+  for (int j = 0; j < 3; ++j) { L.dv1[j] = 0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }
+}
+
+// ------------------------------------------------------------------------------------------
+// env layer
+// ------------------------------------------------------------------------------------------
+// normalize_angle_mpi_pi (jsbsim_gym.py:60-78) on a float32 value (numpy-1.x promotion)
+__device__ __forceinline__ float norm_angle(float a) {
+  if (isnan(a) || isinf(a)) return 0.0f;
+  double x = (double)a;
+  if (!(fabs(x) < 2.0 * PI_D)) x = fmod(x, 2.0 * PI_D);
+  if (x < 0.0) x += 2.0 * PI_D;
+  if (x >= PI_D) x -= 2.0 * PI_D;
+  if (x == 0.0) x = 0.0;
+  return (float)x;
+}
+// _get_current_single_observation (jsbsim_gym.py:172-197)
+__device__ void make_frame(const Lane& L, double ce, double se, float* f) {
+  Derived d;
+  float lat, lon;
+  derive(L, ce, se, d, &lat, &lon);
+  float phi, tht, psi;
+  euler(d.Tl2b, phi, tht, psi);
+  f[0] = (float)((double)lat * 6.3781e6);
+  f[1] = (float)((double)lon * 6.3781e6);
+  f[2] = (float)(d.h_ft * 0.3048);
+  f[3] = L.lx[F16L_MACH];
+  f[4] = L.lx[F16L_ALPHA];
+  f[5] = L.lx[F16L_BETA];
+  f[6] = d.pqr[0]; f[7] = d.pqr[1]; f[8] = d.pqr[2];
+  f[9] = norm_angle(phi); f[10] = norm_angle(tht); f[11] = norm_angle(psi);
+  f[12] = L.goal[0]; f[13] = L.goal[1]; f[14] = L.goal[2];
+}
+__device__ __forceinline__ float norm3f(float a, float b, float c) {
+#pragma clang fp contract(off)
+  float s = a * a;
+  s = s + b * b;
+  s = s + c * c;
+  return sqrtf(s);
+}
+
+struct EnvArgs {
+  int64_t n;
+  int32_t K, down_sample, max_steps, flags;
+  float dg, crash;
+  double gain;
+  uint64_t seed;
+  int64_t id_base;
+};
+
+// reset a lane from the IC template (or a per-lane IC) and produce its frame 0
+__device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const float* goal,
+                           const EnvArgs& E, int64_t k, const float* T, const ModelConsts& C,
+                           float* f0) {
+  const int32_t ep = L.ep_count;
+  if (ic) {
+    apply_ic(L, ic, T, C);
+  } else {
+    lane_load(tmpl, 0, L);
+  }
+  if (goal) {
+    L.goal[0] = goal[0]; L.goal[1] = goal[1]; L.goal[2] = goal[2];
+  } else {
+    rng_goal(E.seed, (uint64_t)(E.id_base + k), (uint32_t)ep, L.goal);
+  }
+  L.ep_count = ep + 1;
+  L.step = 0;
+  L.ep_ret = 0.0;
+  make_frame(L, 1.0, 0.0, f0);
+  L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+#define BLOCK 256
+#define FRAME_PITCH 16
+
+__device__ __forceinline__ void stage_tables(float* sT) {
+  for (int j = threadIdx.x; j < F16_BLOB_FLOATS; j += blockDim.x) sT[j] = F16_BLOB_INIT[j];
+  __syncthreads();
+}
+
+struct StepArgs {
+  SoA s, tmpl;
+  const float* act;
+  const float* obs_prev;
+  float* obs;
+  float* rew;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* tobs;
+  double* ep_ret;
+  int32_t* ep_len;
+  int32_t* done_idx;
+  int32_t* n_done;
+  EnvArgs E;
+  ModelConsts C;
+};
+
+__global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
+  __shared__ float sT[F16_BLOB_FLOATS];
+  __shared__ float sF[BLOCK * FRAME_PITCH];   // final frame per lane
+  __shared__ float sR[BLOCK * FRAME_PITCH];   // reset frame per lane (done lanes)
+  __shared__ int sDone[BLOCK];
+  stage_tables(sT);
+  const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = k < a.E.n;
+  int done = 0;
+  if (live) {
+    Lane L;
+    lane_load(a.s, k, L);
+    const float4 av = reinterpret_cast<const float4*>(a.act)[k];
+    const float cmd[4] = {av.x, av.y, av.z, av.w};
+    L.step += 1;                                              // jsbsim_gym.py:215
+    double ce = cos(L.epa), se = sin(L.epa);
+    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, sT, a.C, false);  // :225-232
+    float f[F16_OBS_DIM];
+    make_frame(L, ce, se, f);                                 // :234
+    // reward / termination (:237-261) in float32, then PositionReward (:493-507)
+    float r32;
+    int te = 0, tr;
+    {
+#pragma clang fp contract(off)
+      double r = 0.0;
+      const float alt = f[2];
+      if (alt < a.E.crash) { r = -10.0; te = 1; }
+      const float dx = f[0] - f[12], dy = f[1] - f[13];
+      float d2 = dx * dx;
+      d2 = d2 + dy * dy;
+      if (!te && sqrtf(d2) < a.E.dg && fabsf(alt - f[14]) < a.E.dg) { r = 10.0; te = 1; }
+      tr = L.step >= a.E.max_steps ? 1 : 0;                 // env :260 | TimeLimit
+      const float dcur = norm3f(f[12] - f[0], f[13] - f[1], f[14] - f[2]);
+      const float ddiff = L.last_d - dcur;
+      r = r + a.E.gain * (double)ddiff;
+      L.last_d = dcur;
+      L.ep_ret += r;                                         // monitor.py:96-99
+      r32 = (float)r;
+    }
+    a.rew[k] = r32;
+    a.term[k] = (uint8_t)te;
+    a.trunc[k] = (uint8_t)tr;
+    done = te | tr;
+#pragma unroll
+    for (int j = 0; j < F16_OBS_DIM; ++j) sF[threadIdx.x * FRAME_PITCH + j] = f[j];
+    if (done) {
+      if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
+      if (a.ep_len) a.ep_len[k] = L.step;
+      if (!(a.E.flags & F16_FLAG_NO_AUTORESET)) {
+        float f0[F16_OBS_DIM];
+        lane_reset(L, a.tmpl, nullptr, nullptr, a.E, k, sT, a.C, f0);
+#pragma unroll
+        for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f0[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f[j];
+      }
+    }
+    lane_store(a.s, k, L);
+  }
+  sDone[threadIdx.x] = done;
+  // compaction of finished lanes (wave64 ballot)
+  if (a.done_idx) {
+    const unsigned long long m = __ballot(done);
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (m) {
+      if (lane == 0) base = atomicAdd(a.n_done, __popcll(m));
+      base = __shfl(base, 0);
+      if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
+    }
+  }
+  __syncthreads();
+  // ordered stack rebuild: each wave copies its 64 rows, row by row, coalesced
+  const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
+  for (int rr = 0; rr < 64; ++rr) {
+    const int64_t row = row0 + rr;
+    if (row >= a.E.n) break;
+    const int li = wave * 64 + rr;
+    const bool d = sDone[li] != 0;
+    const float* prev = a.obs_prev + row * KC;
+    float* out = a.obs + row * KC;
+    if (!d) {
+      for (int c = lane; c < KC; c += 64)
+        out[c] = (c < HC) ? prev[c + F16_OBS_DIM] : sF[li * FRAME_PITCH + (c - HC)];
+    } else {
+      float* tout = a.tobs ? a.tobs + row * KC : nullptr;
+      const bool autoreset = !(a.E.flags & F16_FLAG_NO_AUTORESET);
+      for (int c = lane; c < KC; c += 64) {
+        const float v = (c < HC) ? prev[c + F16_OBS_DIM] : sF[li * FRAME_PITCH + (c - HC)];
+        if (tout) tout[c] = v;
+        out[c] = autoreset ? sR[li * FRAME_PITCH + (c % F16_OBS_DIM)] : v;
+      }
+    }
+  }
+}
+
+struct ResetArgs {
+  SoA s, tmpl;
+  const uint8_t* mask;
+  const float* goals;
+  const double* ic;
+  float* obs;
+  EnvArgs E;
+  ModelConsts C;
+};
+__global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
+  __shared__ float sT[F16_BLOB_FLOATS];
+  stage_tables(sT);
+  const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= a.E.n) return;
+  if (a.mask && !a.mask[k]) return;
+  Lane L;
+  lane_load(a.s, k, L);
+  float f0[F16_OBS_DIM];
+  lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, a.goals ? a.goals + 3 * k : nullptr,
+             a.E, k, sT, a.C, f0);
+  lane_store(a.s, k, L);
+  if (a.obs) {
+    float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;
+    for (int r = 0; r < a.E.K; ++r)
+      for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
+  }
+}
+
+// IC -> state (used once at create to build the reset template, n = 1)
+__global__ void f16_ic_kernel(SoA dst, const double* ic, ModelConsts C) {
+  __shared__ float sT[F16_BLOB_FLOATS];
+  stage_tables(sT);
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Lane L;
+  memset(&L, 0, sizeof L);
+  apply_ic(L, ic, sT, C);
+  L.ep_ret = 0.0; L.step = 0; L.ep_count = 0; L.last_d = 0.0f;
+  L.goal[0] = L.goal[1] = L.goal[2] = 0.0f;
+  lane_store(dst, 0, L);
+}
+
+__global__ void f16_get_state_kernel(SoA s, double* c) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= s.n) return;
+  Lane L;
+  lane_load(s, k, L);
+  double* o = c + (int64_t)F16C_N * k;
+  for (int j = 0; j < 3; ++j) {
+    o[F16C_RI + j] = L.rI[j]; o[F16C_VI + j] = L.vI[j];
+    o[F16C_VIH1 + j] = L.vI[j] + (double)L.dv1[j];
+    o[F16C_VIH2 + j] = L.vI[j] + (double)L.dv2[j];
+    o[F16C_AI + j] = L.aI[j]; o[F16C_AIP + j] = L.aIp[j]; o[F16C_WI + j] = L.wI[j];
+    o[F16C_WID + j] = L.wId[j]; o[F16C_BA + j] = L.ba[j]; o[F16C_GOAL + j] = L.goal[j];
+    o[F16C_WIND + j] = L.wind[j];
+  }
+  for (int j = 0; j < 4; ++j) { o[F16C_Q + j] = L.q[j]; o[F16C_CMD + j] = 0.0; }
+  o[F16C_EPA_C] = cos(L.epa); o[F16C_EPA_S] = sin(L.epa);
+  o[F16C_TEF] = L.tef; o[F16C_AIL] = L.ail; o[F16C_ELE] = L.ele; o[F16C_RUD] = L.rud;
+  o[F16C_LEF] = L.lef; o[F16C_SB] = L.sb;
+  o[F16C_PID_R_I] = L.pri; o[F16C_PID_R_P] = L.prp; o[F16C_PID_P_I] = L.ppi;
+  o[F16C_PID_P_P] = L.ppp; o[F16C_PID_Y_I] = L.pyi; o[F16C_PID_Y_P] = L.pyp;
+  o[F16C_N1] = L.n1; o[F16C_N2] = L.n2; o[F16C_AUG] = (L.flags & LANE_FLAG_AUG) ? 1.0 : 0.0;
+  for (int j = 0; j < F16L_N; ++j) o[F16C_LX + j] = L.lx[j];
+  o[F16C_LAST_D] = L.last_d; o[F16C_STEP] = L.step; o[F16C_EP_RET] = L.ep_ret;
+  o[F16C_EP_COUNT] = (double)(uint32_t)L.ep_count;
+}
+
+__global__ void f16_set_state_kernel(SoA s, const double* c) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= s.n) return;
+  Lane L;
+  const double* o = c + (int64_t)F16C_N * k;
+  for (int j = 0; j < 3; ++j) {
+    L.rI[j] = o[F16C_RI + j]; L.vI[j] = o[F16C_VI + j];
+    L.dv1[j] = (float)(o[F16C_VIH1 + j] - o[F16C_VI + j]);
+    L.dv2[j] = (float)(o[F16C_VIH2 + j] - o[F16C_VI + j]);
+    L.aI[j] = (float)o[F16C_AI + j]; L.aIp[j] = (float)o[F16C_AIP + j]; L.wI[j] = (float)o[F16C_WI + j];
+    L.wId[j] = (float)o[F16C_WID + j]; L.ba[j] = (float)o[F16C_BA + j]; L.goal[j] = (float)o[F16C_GOAL + j];
+    L.wind[j] = (float)o[F16C_WIND + j];
+  }
+  for (int j = 0; j < 4; ++j) L.q[j] = (float)o[F16C_Q + j];
+  L.epa = atan2(o[F16C_EPA_S], o[F16C_EPA_C]);
+  L.tef = (float)o[F16C_TEF]; L.ail = (float)o[F16C_AIL]; L.ele = (float)o[F16C_ELE];
+  L.rud = (float)o[F16C_RUD]; L.lef = (float)o[F16C_LEF]; L.sb = (float)o[F16C_SB];
+  L.pri = (float)o[F16C_PID_R_I]; L.prp = (float)o[F16C_PID_R_P]; L.ppi = (float)o[F16C_PID_P_I];
+  L.ppp = (float)o[F16C_PID_P_P]; L.pyi = (float)o[F16C_PID_Y_I]; L.pyp = (float)o[F16C_PID_Y_P];
+  L.n1 = (float)o[F16C_N1]; L.n2 = (float)o[F16C_N2];
+  L.flags = o[F16C_AUG] != 0.0 ? LANE_FLAG_AUG : 0;
+  for (int j = 0; j < F16L_N; ++j) L.lx[j] = (float)o[F16C_LX + j];
+  L.last_d = (float)o[F16C_LAST_D]; L.step = (int32_t)o[F16C_STEP]; L.ep_ret = o[F16C_EP_RET];
+  L.ep_count = (int32_t)(uint32_t)o[F16C_EP_COUNT];
+  lane_store(s, k, L);
+}
+
+// Trim: Newton on (alpha, elevator cmd, throttle cmd), mirrors oracle trim_one()
+__device__ void trim_residual(const double* icb, const float* x, const float* T, const ModelConsts& C,
+                              float* res) {
+  double ic[F16_IC_N];
+  for (int j = 0; j < F16_IC_N; ++j) ic[j] = icb[j];
+  const double vt = icb[F16_IC_U_FPS];
+  ic[F16_IC_U_FPS] = vt * cos((double)x[0]);
+  ic[F16_IC_V_FPS] = 0.0;
+  ic[F16_IC_W_FPS] = vt * sin((double)x[0]);
+  ic[F16_IC_THETA_RAD] = x[0];
+  ic[F16_IC_PHI_RAD] = 0.0;
+  ic[F16_IC_P_RPS] = ic[F16_IC_Q_RPS] = ic[F16_IC_R_RPS] = 0.0;
+  ic[F16_IC_CMD_AIL] = 0.0; ic[F16_IC_CMD_RUD] = 0.0;
+  ic[F16_IC_CMD_ELE] = x[1];
+  ic[F16_IC_CMD_THR] = x[2];
+  Lane L;
+  apply_ic(L, ic, T, C);
+  Derived d;
+  derive(L, 1.0, 0.0, d);
+  float gb[3];
+  mvec(d.Tec2b, d.gE, gb);
+  res[0] = L.ba[0] + gb[0];
+  res[1] = L.ba[2] + gb[2];
+  res[2] = L.wId[1];
+}
+__device__ void inv3f(const float* M, float* I, bool& ok) {
+  const float a = M[0], b = M[1], c = M[2], d = M[3], e = M[4], f = M[5], g = M[6], h = M[7], k = M[8];
+  const float A = e * k - f * h, B = -(d * k - f * g), Cc = d * h - e * g;
+  const float det = a * A + b * B + c * Cc;
+  ok = det != 0.0f;
+  const float r = ok ? 1.0f / det : 0.0f;
+  I[0] = A * r; I[1] = -(b * k - c * h) * r; I[2] = (b * f - c * e) * r;
+  I[3] = B * r; I[4] = (a * k - c * g) * r; I[5] = -(a * f - c * d) * r;
+  I[6] = Cc * r; I[7] = -(a * h - b * g) * r; I[8] = (a * e - b * d) * r;
+}
+__global__ __launch_bounds__(BLOCK) void f16_trim_kernel(int64_t n, const double* ic_in, double* ic_out,
+                                                         double* resid, ModelConsts C) {
+  __shared__ float sT[F16_BLOB_FLOATS];
+  stage_tables(sT);
+  const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= n) return;
+  const double* icb = ic_in + (int64_t)F16_IC_N * k;
+  float x[3] = {0.05f, 0.0f, 0.5f};
+  const float hs[3] = {1e-3f, 1e-3f, 1e-3f};
+  float r[3];
+  for (int it = 0; it < 12; ++it) {
+    trim_residual(icb, x, sT, C, r);
+    float Jm[9], Ji[9];
+    for (int j = 0; j < 3; ++j) {
+      float xp[3] = {x[0], x[1], x[2]}, rp[3];
+      xp[j] += hs[j];
+      trim_residual(icb, xp, sT, C, rp);
+      for (int i = 0; i < 3; ++i) Jm[3 * i + j] = (rp[i] - r[i]) / hs[j];
+    }
+    bool ok;
+    inv3f(Jm, Ji, ok);
+    if (!ok) break;
+    float dx[3];
+    mvec(Ji, r, dx);
+    for (int i = 0; i < 3; ++i) x[i] -= dx[i];
+    x[0] = clipf(x[0], -0.3f, 0.6f);
+    x[1] = clipf(x[1], -1.0f, 0.44f);
+    x[2] = clipf(x[2], 0.0f, 1.0f);
+  }
+  trim_residual(icb, x, sT, C, r);
+  double* o = ic_out + (int64_t)F16_IC_N * k;
+  for (int j = 0; j < F16_IC_N; ++j) o[j] = icb[j];
+  const double vt = icb[F16_IC_U_FPS];
+  o[F16_IC_U_FPS] = vt * cos((double)x[0]);
+  o[F16_IC_V_FPS] = 0.0;
+  o[F16_IC_W_FPS] = vt * sin((double)x[0]);
+  o[F16_IC_THETA_RAD] = x[0];
+  o[F16_IC_PHI_RAD] = 0.0;
+  o[F16_IC_P_RPS] = o[F16_IC_Q_RPS] = o[F16_IC_R_RPS] = 0.0;
+  o[F16_IC_CMD_AIL] = 0.0; o[F16_IC_CMD_RUD] = 0.0;
+  o[F16_IC_CMD_ELE] = x[1];
+  o[F16_IC_CMD_THR] = x[2];
+  if (resid)
+    for (int i = 0; i < 3; ++i) resid[3 * k + i] = fabsf(r[i]);
+}
+
+__global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t seed, uint64_t step, float* act) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint64_t gid = (uint64_t)(id_base + k);
+  uint32_t o[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step,
+         (uint32_t)(step >> 32), o);
+  const float lo[4] = {-1.f, -1.f, -1.f, 0.f}, hi[4] = {1.f, 1.f, 1.f, 1.f};
+  float4 v;
+  float* pv = &v.x;
+  for (int j = 0; j < 4; ++j) {
+    const float u = (float)(o[j] >> 8) * (1.0f / 16777216.0f);
+    pv[j] = lo[j] + (hi[j] - lo[j]) * u;
+  }
+  reinterpret_cast<float4*>(act)[k] = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct f16env {
+  f16env_config cfg;
+  int device;
+  void* mem;       // state SoA
+  void* tmem;      // template SoA (n = 1)
+  double* ic_dev;  // default IC
+  SoA soa, tmpl;
+  ModelConsts C;
+  size_t bytes;
+};
+
+static void soa_carve(void* base, int64_t n, SoA& s) {
+  char* p = (char*)base;
+  s.n = n;
+  s.d = (double*)p;
+  p += sizeof(double) * NDF * n;
+  s.f = (float*)p;
+  p += sizeof(float) * NFF * n;
+  s.i = (int32_t*)p;
+}
+static size_t soa_bytes(int64_t n) { return (size_t)n * (NDF * 8 + NFF * 4 + NIF * 4); }
+
+// Same mass-balance / constants derivation as oracle init_consts() (f16.xml:37-83,245-300).
+static void build_consts(const f16env_config& cfg, ModelConsts& C) {
+  const double SLUG2LB = 32.174049, IN2FT = 1.0 / 12.0;
+  const double empty = 17400.0, cg_e[3] = {-193.0, 0.0, -5.1};
+  const double pilot = 230.0, pilot_loc[3] = {-336.2, 0.0, 0.0};
+  const double tank_w[4] = {1000.0, 1000.0, 0.0, 0.0};
+  const double tank_loc[4][3] = {{-174.4, 65.0, 5.0}, {-174.4, -65.0, 5.0}, {-174.4, 65.0, -15.0}, {-174.4, -65.0, -15.0}};
+  double W = empty + pilot, m[3], cg[3];
+  for (int i = 0; i < 3; ++i) m[i] = empty * cg_e[i] + pilot * pilot_loc[i];
+  for (int t = 0; t < 4; ++t) {
+    W += tank_w[t];
+    for (int i = 0; i < 3; ++i) m[i] += tank_w[t] * tank_loc[t][i];
+  }
+  for (int i = 0; i < 3; ++i) cg[i] = m[i] / W;
+  const double mass = W / SLUG2LB;
+  double J[9] = {9496, 0, -982, 0, 55814, 0, -982, 0, 63100};
+  auto s2b = [&](const double* r, double* o) {
+    o[0] = IN2FT * (cg[0] - r[0]); o[1] = IN2FT * (r[1] - cg[1]); o[2] = IN2FT * (cg[2] - r[2]);
+  };
+  auto pm = [&](double mm, const double* v) {
+    const double sv[3] = {mm * v[0], mm * v[1], mm * v[2]};
+    const double xx = sv[0] * v[0], yy = sv[1] * v[1], zz = sv[2] * v[2];
+    const double xy = -sv[0] * v[1], xz = -sv[0] * v[2], yz = -sv[1] * v[2];
+    J[0] += yy + zz; J[1] += xy; J[2] += xz; J[3] += xy; J[4] += xx + zz; J[5] += yz;
+    J[6] += xz; J[7] += yz; J[8] += xx + yy;
+  };
+  double v[3];
+  s2b(pilot_loc, v);
+  pm(pilot / SLUG2LB, v);
+  for (int t = 0; t < 4; ++t) { s2b(tank_loc[t], v); pm(tank_w[t] / SLUG2LB, v); }
+  const double a = J[0], b = J[1], c = J[2], d = J[3], e = J[4], f = J[5], g = J[6], h = J[7], k = J[8];
+  const double A = e * k - f * h, B = -(d * k - f * g), Cc = d * h - e * g;
+  const double det = a * A + b * B + c * Cc, r = 1.0 / det;
+  const double Ji[9] = {A * r, -(b * k - c * h) * r, (b * f - c * e) * r, B * r, (a * k - c * g) * r,
+                        -(a * f - c * d) * r, Cc * r, -(a * h - b * g) * r, (a * e - b * d) * r};
+  C.inv_mass = (float)(1.0 / mass);
+  for (int i = 0; i < 9; ++i) { C.J[i] = (float)J[i]; C.Jinv[i] = (float)Ji[i]; }
+  const double aerorp[3] = {-189.5, 0.0, 3.9}, eye[3] = {-336.2, 0.0, 29.5}, eng[3] = {0, 0, 0};
+  s2b(aerorp, v); for (int i = 0; i < 3; ++i) C.rp[i] = (float)v[i];
+  s2b(eye, v); for (int i = 0; i < 3; ++i) C.eye[i] = (float)v[i];
+  s2b(eng, v); for (int i = 0; i < 3; ++i) C.eng[i] = (float)v[i];
+  C.inv_gref = (float)((WGS_A * WGS_A) / GM_E);
+  // US-76 sea level in JSBSim units
+  const double R = 8.31432 / 0.0289644;
+  C.rho_sl = (float)(101325.0 / (R * 288.15) / 515.3788183931961);
+  C.a_sl = (float)(sqrt(1.4 * R * 288.15) / 0.3048);
+  C.p_sl = (float)(101325.0 / 47.88025898033584);
+  C.kts_per_fps = (float)(1.0 / (1852.0 / (3600.0 * 0.3048)));
+  C.dt = cfg.dt;
+  C.cos_dE = cos(OMEGA_E * cfg.dt);
+  C.sin_dE = sin(OMEGA_E * cfg.dt);
+}
+
+static EnvArgs env_args(const f16env* h) {
+  EnvArgs E;
+  E.n = h->cfg.n_envs;
+  E.K = h->cfg.stack_k;
+  E.down_sample = h->cfg.down_sample;
+  E.max_steps = h->cfg.max_steps;
+  E.flags = h->cfg.flags;
+  E.dg = (float)h->cfg.dg_m;
+  E.crash = (float)h->cfg.crash_alt_m;
+  E.gain = h->cfg.goal_gain;
+  E.seed = h->cfg.seed;
+  E.id_base = h->cfg.env_id_base;
+  return E;
+}
+
+extern "C" {
+
+int f16env_config_default(f16env_config* c) {
+  if (!c) return set_err(-1, "null config");
+  memset(c, 0, sizeof *c);
+  c->n_envs = 1;
+  c->stack_k = 10;
+  c->down_sample = 4;
+  c->max_steps = 1200;
+  c->dt = 1.0 / 120.0;
+  c->dg_m = 100.0;
+  c->goal_gain = 1e-2;
+  c->crash_alt_m = 10.0;
+  c->ic[F16_IC_H_SL_FT] = 5000.0;
+  c->ic[F16_IC_U_FPS] = 900.0;
+  return 0;
+}
+
+int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
+  if (!cfg || !out) return set_err(-1, "null argument");
+  if (cfg->n_envs <= 0) return set_err(-1, "n_envs must be > 0");
+  if (cfg->stack_k < 1 || cfg->stack_k > 64) return set_err(-1, "stack_k must be in [1, 64]");
+  if (cfg->down_sample < 0) return set_err(-1, "down_sample must be >= 0");
+  if (!(cfg->dt > 0.0)) return set_err(-1, "dt must be > 0");
+  HIPCHK(hipSetDevice(device));
+  f16env* h = new f16env();
+  h->cfg = *cfg;
+  h->device = device;
+  build_consts(*cfg, h->C);
+  h->bytes = soa_bytes(cfg->n_envs);
+  hipError_t e = hipMalloc(&h->mem, h->bytes);
+  if (e != hipSuccess) { delete h; return set_err(-3, "hipMalloc(state) failed"); }
+  hipMemset(h->mem, 0, h->bytes);
+  soa_carve(h->mem, cfg->n_envs, h->soa);
+  if (hipMalloc(&h->tmem, soa_bytes(1)) != hipSuccess || hipMalloc((void**)&h->ic_dev, sizeof(double) * F16_IC_N) != hipSuccess) {
+    hipFree(h->mem); delete h;
+    return set_err(-3, "hipMalloc(template) failed");
+  }
+  soa_carve(h->tmem, 1, h->tmpl);
+  hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(f16_ic_kernel, dim3(1), dim3(BLOCK), 0, 0, h->tmpl, (const double*)h->ic_dev, h->C);
+  e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) {
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
+    return set_err(-2, hipGetErrorString(e));
+  }
+  *out = h;
+  return 0;
+}
+
+int f16env_destroy(f16env_t h) {
+  if (!h) return 0;
+  hipSetDevice(h->device);
+  hipFree(h->mem);
+  hipFree(h->tmem);
+  hipFree(h->ic_dev);
+  delete h;
+  return 0;
+}
+
+size_t f16env_state_bytes(f16env_t h) { return h ? h->bytes : 0; }
+int f16env_state_bytes_per_env(void) { return STATE_BYTES; }
+
+static inline unsigned nblocks(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+
+int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic, float* obs) {
+  if (!h) return set_err(-1, "null handle");
+  ResetArgs a;
+  a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = obs;
+  a.E = env_args(h);
+  a.C = h->C;
+  hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_prev, float* obs, float* rew,
+                uint8_t* terminated, uint8_t* truncated, float* terminal_obs, double* ep_return, int32_t* ep_len,
+                int32_t* done_idx, int32_t* n_done) {
+  if (!h) return set_err(-1, "null handle");
+  if (!act || !obs_prev || !obs || !rew || !terminated || !truncated)
+    return set_err(-1, "act/obs_prev/obs/rew/terminated/truncated are required");
+  if (done_idx && !n_done) return set_err(-1, "done_idx requires n_done");
+  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  StepArgs a;
+  a.s = h->soa; a.tmpl = h->tmpl; a.act = act; a.obs_prev = obs_prev; a.obs = obs; a.rew = rew;
+  a.term = terminated; a.trunc = truncated; a.tobs = terminal_obs; a.ep_ret = ep_return; a.ep_len = ep_len;
+  a.done_idx = done_idx; a.n_done = n_done;
+  a.E = env_args(h);
+  a.C = h->C;
+  if (n_done) HIPCHK(hipMemsetAsync(n_done, 0, sizeof(int32_t), (hipStream_t)stream));
+  hipLaunchKernelGGL(f16_step_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_get_state(f16env_t h, void* stream, double* canon) {
+  if (!h || !canon) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_get_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_set_state(f16env_t h, void* stream, const double* canon) {
+  if (!h || !canon) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_trim(f16env_t h, void* stream, const double* ic_in, double* ic_out, double* residual_out) {
+  if (!h || !ic_in || !ic_out) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_trim_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream,
+                     (int64_t)h->soa.n, ic_in, ic_out, residual_out, h->C);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step, float* act) {
+  if (!h || !act) return set_err(-1, "null argument");
+  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  hipLaunchKernelGGL(f16_sample_actions_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream,
+                     (int64_t)h->soa.n, (int64_t)h->cfg.env_id_base, seed, step, act);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+const char* f16env_step_kernel_name(void) { return "f16_step_kernel"; }
+
+double f16env_algorithmic_bytes_per_env_step(int stack_k) {
+  return 16.0 + 60.0 * stack_k + 60.0 * (stack_k - 1) + 4.0 + 2.0 + 2.0 * STATE_BYTES;
+}
+
+const char* f16env_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

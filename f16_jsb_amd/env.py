@@ -1,0 +1,314 @@
+"""Host side of the MI355X F-16 environment.
+
+``F16Envs``   -- thin owner of one libf16env handle: device tensors in, device tensors out
+                 (the throughput path; no per-step allocation, no host sync).
+``F16VecEnv`` -- drop-in for the reference's VecEnv boundary
+                 (stable_baselines3/common/vec_env/base_vec_env.py:50-357 VecEnv ABC,
+                 dummy_vec_env.py:56-83 auto-reset / info contract, monitor.py:85-111
+                 episode stats) over ``F16Envs``, returning numpy like DummyVecEnv.
+``reference_goal`` -- jsbsim_gym.py:312-323 with numpy's default_rng(seed), used for
+                 seeded resets so seeded goals match the reference bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from collections import namedtuple
+from copy import deepcopy
+from typing import Any, Optional, Sequence
+
+import numpy as np
+
+from . import spaces
+from ._lib import F16EnvError, check, lib
+from .abi import (F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_NO_AUTORESET, EnvConfig,
+                  algorithmic_bytes_per_env_step, config_default)
+
+StepOut = namedtuple("StepOut", "obs rew terminated truncated terminal_obs ep_return ep_len")
+
+
+def reference_goal(seed) -> np.ndarray:
+    """Goal of JSBSimEnv.reset(seed) (jsbsim_gym.py:312-323), float32 (x, y, alt)."""
+    rng = np.random.default_rng(seed)
+    distance_m = rng.uniform(1000.0, 10000.0)
+    bearing_rad = rng.uniform(0, 2 * np.pi)
+    altitude_m = rng.uniform(1000.0, 4000.0)
+    g = np.zeros(3, dtype=np.float32)
+    g[0] = distance_m * np.cos(bearing_rad)
+    g[1] = distance_m * np.sin(bearing_rad)
+    g[2] = altitude_m
+    return g
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+class F16Envs:
+    """N F-16 envs on one GPU behind the C ABI. All tensors are torch tensors on ``device``."""
+
+    def __init__(self, n_envs: int, stack_k: int = 10, device=None, seed: int = 0,
+                 env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
+                 autoreset: bool = True, ic=None, **cfg_kw):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise F16EnvError("F16Envs needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.torch = torch
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise F16EnvError("device must be a cuda (ROCm) device, got %s" % self.device)
+        self.n = int(n_envs)
+        self.k = int(stack_k)
+        flags = 0 if autoreset else F16_FLAG_NO_AUTORESET
+        self.cfg: EnvConfig = config_default(n_envs=n_envs, stack_k=stack_k, seed=seed, env_id_base=env_id_base,
+                                             max_steps=max_steps, down_sample=down_sample, flags=flags, ic=ic,
+                                             **cfg_kw)
+        L = lib()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(L.f16env_create(ctypes.byref(self.cfg), self.device.index or 0, ctypes.byref(h)), "f16env_create")
+        self._h = h
+        f32, dev = torch.float32, self.device
+        n, k = self.n, self.k
+        self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
+        self._cur = 0
+        self.rew = torch.zeros(n, dtype=f32, device=dev)
+        self.term = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.terminal_obs = torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev)
+        self.ep_return = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self._act = torch.zeros((n, 4), dtype=f32, device=dev)
+
+    # --------------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def obs(self):
+        return self._obs[self._cur]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().f16env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def state_bytes_per_env(self) -> int:
+        return int(lib().f16env_state_bytes_per_env())
+
+    def algorithmic_bytes_per_env_step(self) -> int:
+        return algorithmic_bytes_per_env_step(self.k, self.state_bytes_per_env)
+
+    # --------------------------------------------------------------------------------------
+    def reset(self, mask=None, goals=None, ic=None):
+        """Reset lanes (mask: bool/uint8 (N,) or None=all). goals (N,3) float32 or None
+        (device RNG); ic (N, F16_IC_N) float64 or None (config IC). Returns obs (N,K,15)."""
+        t = self.torch
+        m = None if mask is None else t.as_tensor(mask, device=self.device).to(t.uint8).contiguous()
+        g = None if goals is None else t.as_tensor(goals, device=self.device, dtype=t.float32).contiguous()
+        c = None if ic is None else t.as_tensor(ic, device=self.device, dtype=t.float64).contiguous()
+        if g is not None and tuple(g.shape) != (self.n, 3):
+            raise ValueError("goals must be (N, 3)")
+        if c is not None and tuple(c.shape) != (self.n, F16_IC_N):
+            raise ValueError("ic must be (N, %d)" % F16_IC_N)
+        out = self._obs[self._cur]
+        check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
+        return out
+
+    def step(self, actions) -> StepOut:
+        """One env step for all lanes; ``actions`` (N,4) float32 device tensor (or host
+        array, copied). Returns device tensors; obs alternates between two buffers."""
+        t = self.torch
+        if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
+                and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
+            act = actions
+        else:
+            self._act.copy_(t.as_tensor(actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
+            act = self._act
+        if tuple(act.shape) != (self.n, 4):
+            raise ValueError("actions must be (N, 4), got %s" % (tuple(act.shape),))
+        prev = self._obs[self._cur]
+        nxt = self._obs[self._cur ^ 1]
+        check(lib().f16env_step(self._h, self._stream(), _ptr(act), _ptr(prev), _ptr(nxt), _ptr(self.rew),
+                                _ptr(self.term), _ptr(self.trunc), _ptr(self.terminal_obs),
+                                _ptr(self.ep_return), _ptr(self.ep_len), None, None), "f16env_step")
+        self._cur ^= 1
+        return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
+
+    def get_state(self):
+        s = self.torch.zeros((self.n, F16C_N), dtype=self.torch.float64, device=self.device)
+        check(lib().f16env_get_state(self._h, self._stream(), _ptr(s)), "f16env_get_state")
+        return s
+
+    def set_state(self, canon):
+        s = self.torch.as_tensor(canon, dtype=self.torch.float64, device=self.device).contiguous()
+        if tuple(s.shape) != (self.n, F16C_N):
+            raise ValueError("state must be (N, %d)" % F16C_N)
+        check(lib().f16env_set_state(self._h, self._stream(), _ptr(s)), "f16env_set_state")
+        self.torch.cuda.current_stream(self.device).synchronize()
+
+    def set_obs(self, obs):
+        self._obs[self._cur].copy_(self.torch.as_tensor(obs, dtype=self.torch.float32))
+
+    def trim(self, ic):
+        t = self.torch
+        c = t.as_tensor(ic, dtype=t.float64, device=self.device).contiguous()
+        out = t.zeros_like(c)
+        res = t.zeros((self.n, 3), dtype=t.float64, device=self.device)
+        check(lib().f16env_trim(self._h, self._stream(), _ptr(c), _ptr(out), _ptr(res)), "f16env_trim")
+        return out, res
+
+    def sample_actions(self, seed: int, step: int, out=None):
+        if out is None:
+            out = self.torch.empty((self.n, 4), dtype=self.torch.float32, device=self.device)
+        check(lib().f16env_sample_actions(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                          int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(out)), "f16env_sample_actions")
+        return out
+
+
+class F16VecEnv:
+    """Vectorised drop-in for ``DummyVecEnv([lambda: Monitor(gym.make("JSBSim-v0"))] * N)``.
+
+    Honours the SB3 VecEnv contract (base_vec_env.py:50-357): ``reset() -> obs``,
+    ``step_async/step_wait -> (obs, rews, dones, infos)``, auto-reset with
+    ``infos[i]["terminal_observation"]`` and ``infos[i]["TimeLimit.truncated"]``
+    (dummy_vec_env.py:56-73), Monitor's ``infos[i]["episode"] = {r, l, t}``
+    (monitor.py:96-109), ``seed()`` applied at the next reset (:292-309).
+    ``return_numpy=False`` keeps everything on the GPU (infos list is then omitted: the
+    caller reads ``last_step`` device tensors)."""
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
+                 return_numpy: bool = True, env_id_base: int = 0, **kw):
+        self.num_envs = int(num_envs)
+        self.envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, env_id_base=env_id_base, **kw)
+        self.observation_space = spaces.observation_space(stack_k)
+        self.action_space = spaces.action_space()
+        self.render_mode = None
+        self.return_numpy = bool(return_numpy)
+        self.reset_infos: list = [{} for _ in range(self.num_envs)]
+        self._seeds: list = [None for _ in range(self.num_envs)]
+        self._options: list = [{} for _ in range(self.num_envs)]
+        self._actions = None
+        self._t_start = time.time()
+        self.last_step: Optional[StepOut] = None
+        self._attrs: dict = {}
+
+    # -- VecEnv API -------------------------------------------------------------------------
+    def reset(self):
+        goals = None
+        if any(s is not None for s in self._seeds):
+            # seeded lanes follow the reference's numpy stream; unseeded lanes use the device RNG
+            dev_goals = None
+            if not all(s is not None for s in self._seeds):
+                self.envs.reset()  # draw device goals for every lane first
+                dev_goals = self.envs.get_state()[:, 62:65].float().cpu().numpy()
+            goals = np.zeros((self.num_envs, 3), np.float32)
+            for i, s in enumerate(self._seeds):
+                goals[i] = reference_goal(s) if s is not None else dev_goals[i]
+        obs = self.envs.reset(goals=goals)
+        self._seeds = [None for _ in range(self.num_envs)]
+        self._options = [{} for _ in range(self.num_envs)]
+        self.reset_infos = [{} for _ in range(self.num_envs)]
+        return obs.cpu().numpy() if self.return_numpy else obs
+
+    def step_async(self, actions) -> None:
+        self._actions = actions
+
+    def step_wait(self):
+        out = self.envs.step(self._actions)
+        self.last_step = out
+        if not self.return_numpy:
+            dones = (out.terminated | out.truncated).bool()
+            return out.obs, out.rew, dones, None
+        obs = out.obs.cpu().numpy()
+        rew = out.rew.cpu().numpy()
+        term = out.terminated.cpu().numpy().astype(bool)
+        trunc = out.truncated.cpu().numpy().astype(bool)
+        dones = term | trunc
+        infos = [{"TimeLimit.truncated": False} for _ in range(self.num_envs)]
+        idx = np.flatnonzero(dones)
+        if idx.size:
+            tobs = out.terminal_obs[idx].cpu().numpy()
+            eret = out.ep_return[idx].cpu().numpy()
+            elen = out.ep_len[idx].cpu().numpy()
+            t = round(time.time() - self._t_start, 6)
+            for j, i in enumerate(idx):
+                infos[i]["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
+                infos[i]["terminal_observation"] = tobs[j]
+                infos[i]["episode"] = {"r": round(float(eret[j]), 6), "l": int(elen[j]), "t": t}
+        return obs, rew, dones, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self) -> None:
+        self.envs.close()
+
+    def seed(self, seed: Optional[int] = None) -> Sequence[Optional[int]]:
+        if seed is None:
+            seed = int(np.random.randint(0, np.iinfo(np.uint32).max, dtype=np.uint32))
+        self._seeds = [seed + idx for idx in range(self.num_envs)]
+        return self._seeds
+
+    def set_options(self, options=None) -> None:
+        if options is None:
+            options = {}
+        self._options = deepcopy([options] * self.num_envs) if isinstance(options, dict) else deepcopy(options)
+
+    def _indices(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+    def get_attr(self, attr_name: str, indices=None) -> list:
+        if attr_name in self._attrs:
+            v = self._attrs[attr_name]
+        elif attr_name in ("render_mode", "observation_space", "action_space", "metadata"):
+            v = getattr(self, attr_name)
+        elif attr_name == "spec":
+            v = None
+        else:
+            raise AttributeError(attr_name)
+        return [v for _ in self._indices(indices)]
+
+    def set_attr(self, attr_name: str, value: Any, indices=None) -> None:
+        self._attrs[attr_name] = value
+
+    def env_method(self, method_name: str, *method_args, indices=None, **method_kwargs) -> list:
+        raise AttributeError("F16VecEnv lanes expose no per-env methods (%s)" % method_name)
+
+    def env_is_wrapped(self, wrapper_class, indices=None) -> list:
+        name = getattr(wrapper_class, "__name__", str(wrapper_class))
+        # Monitor / TimeLimit / PositionReward semantics are built into the kernel
+        wrapped = name in ("Monitor", "TimeLimit", "PositionReward")
+        return [wrapped for _ in self._indices(indices)]
+
+    def has_attr(self, attr_name: str) -> bool:
+        try:
+            self.get_attr(attr_name)
+            return True
+        except AttributeError:
+            return False
+
+    def get_images(self):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md component #9)")
+
+    def render(self, mode: Optional[str] = None):
+        return None
+
+    @property
+    def unwrapped(self):
+        return self

@@ -1,0 +1,190 @@
+/*
+ * f16env.h -- C ABI of the MI355X-native vectorised F-16 environment (libf16env.so).
+ *
+ * One handle = one device = N independent F-16 envs held as struct-of-arrays state in
+ * HBM. Every array argument is a caller-owned DEVICE pointer (e.g. a PyTorch-ROCm
+ * tensor's data_ptr()); `stream` is a hipStream_t (NULL = default stream). Calls are
+ * stream-ordered and asynchronous unless documented otherwise. A handle is not
+ * thread-safe. Errors: int status (0 ok, <0 error) + f16env_last_error() (thread-local).
+ *
+ * What each entry point replaces in the reference (Soham4001A/F16_JSB):
+ *   f16env_create   <- jsbsim_gym/jsbsim_gym.py:122-164 JSBSimEnv.__init__ (FGFDMExec(root),
+ *                      load_model('f16'), _set_initial_conditions :166-170, run_ic :155)
+ *                      x N, plus stable_baselines3/common/vec_env/dummy_vec_env.py:30-50
+ *   f16env_reset    <- jsbsim_gym.py:289-331 JSBSimEnv.reset + :511-519 PositionReward.reset,
+ *                      vectorised as dummy_vec_env.py:75-83 DummyVecEnv.reset
+ *   f16env_step     <- jsbsim_gym.py:199-287 JSBSimEnv.step (4x FGFDMExec.run() :225-232),
+ *                      :487-509 PositionReward.step, gymnasium TimeLimit(1200) (:537-545),
+ *                      common/monitor.py:85-111 Monitor.step and the auto-reset loop of
+ *                      dummy_vec_env.py:56-73 DummyVecEnv.step_wait
+ *   f16env_get_state/set_state <- FGFDMExec state (no reference equivalent; used for
+ *                      parity replay and checkpoint/restore)
+ *   f16env_trim     <- no reference equivalent (the reference never trims; BASELINE cfg 2)
+ *   f16env_sample_actions <- action_space.sample() (jsbsim_gym.py:575), device Philox
+ */
+#ifndef F16ENV_H
+#define F16ENV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define F16ENV_ABI_VERSION 1
+
+/* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
+#define F16_OBS_DIM 15
+#define F16_ACT_DIM 4
+
+/* Initial condition vector (per env), JSBSim "ic/" semantics (jsbsim_gym.py:166-170). */
+enum f16_ic_index {
+  F16_IC_LAT_GEOD_RAD = 0, /* geodetic latitude                         (default 0)    */
+  F16_IC_LON_RAD,          /* longitude                                 (default 0)    */
+  F16_IC_H_SL_FT,          /* altitude above the WGS84 ellipsoid        (5000)         */
+  F16_IC_U_FPS,            /* body velocity wrt ECEF: u (ic/u-fps)     (900)          */
+  F16_IC_V_FPS,            /*                          v                (0)            */
+  F16_IC_W_FPS,            /*                          w                (0)            */
+  F16_IC_PHI_RAD,          /* Euler angles wrt local NED                (0)            */
+  F16_IC_THETA_RAD,
+  F16_IC_PSI_RAD,
+  F16_IC_P_RPS,            /* body rates wrt ECEF                       (0)            */
+  F16_IC_Q_RPS,
+  F16_IC_R_RPS,
+  F16_IC_CMD_AIL,          /* FCS command properties held at IC         (0)            */
+  F16_IC_CMD_ELE,
+  F16_IC_CMD_RUD,
+  F16_IC_CMD_THR,
+  F16_IC_WIND_N_FPS,       /* steady wind NED (cfg5; the reference has none) (0)       */
+  F16_IC_WIND_E_FPS,
+  F16_IC_WIND_D_FPS,
+  F16_IC_N
+};
+
+/* Canonical full per-env state (fp64 vector). Both the HIP path and the CPU oracle can
+ * export/import it; the HIP path stores most of it in fp32 SoA. */
+enum f16_canon_index {
+  F16C_RI = 0,       /* 0-2   inertial position ECI (ft)                                */
+  F16C_VI = 3,       /* 3-5   inertial velocity ECI (ft/s)                              */
+  F16C_VIH1 = 6,     /* 6-8   AB3 history: inertial velocity one frame back            */
+  F16C_VIH2 = 9,     /* 9-11  two frames back                                          */
+  F16C_AI = 12,      /* 12-14 latest inertial acceleration (FGAccelerations vUVWidot)   */
+  F16C_AIP = 15,     /* 15-17 AB2 history: previous inertial acceleration             */
+  F16C_Q = 18,       /* 18-21 attitude quaternion ECI->body (q0 q1 q2 q3)              */
+  F16C_WI = 22,      /* 22-24 body rates wrt ECI, body axes (vPQRi)                    */
+  F16C_WID = 25,     /* 25-27 latest vPQRidot                                          */
+  F16C_BA = 28,      /* 28-30 latest body specific-force acceleration (vBodyAccel)     */
+  F16C_EPA_C = 31,   /* cos / sin of the Earth position angle                          */
+  F16C_EPA_S = 32,
+  F16C_TEF = 33,     /* fcs/tef-control            (kinematic, f16.xml:334-350)        */
+  F16C_AIL = 34,     /* fcs/left-aileron-pos-norm  (kinematic, f16.xml:419-432)        */
+  F16C_ELE = 35,     /* fcs/elevator-pos-norm      (kinematic, f16.xml:630-643)        */
+  F16C_RUD = 36,     /* fcs/rudder-pos-norm        (kinematic, f16.xml:739-752)        */
+  F16C_LEF = 37,     /* fcs/lef-control            (kinematic, f16.xml:831-843)        */
+  F16C_SB = 38,      /* fcs/speedbrake-pos-deg     (kinematic, f16.xml:909-922)        */
+  F16C_PID_R_I = 39, /* roll-rate-pid  (f16.xml:383-389): integrator, previous input   */
+  F16C_PID_R_P = 40,
+  F16C_PID_P_I = 41, /* g-load-pid     (f16.xml:594-604)                               */
+  F16C_PID_P_P = 42,
+  F16C_PID_Y_I = 43, /* yaw-load-pid   (f16.xml:716-727)                               */
+  F16C_PID_Y_P = 44,
+  F16C_N1 = 45,      /* FGTurbine N1, N2 (%), augmentation flag                         */
+  F16C_N2 = 46,
+  F16C_AUG = 47,
+  F16C_LX = 48,      /* 48-57 auxiliary latch read by the next frame's FCS:             */
+                     /* alpha, beta, mach, vc_kts, vg_fps, p_aero, q_aero, r_aero,      */
+                     /* n_pilot_y, n_pilot_z                                           */
+  F16C_CMD = 58,     /* 58-61 fcs/{aileron,elevator,rudder,throttle}-cmd-norm          */
+  F16C_GOAL = 62,    /* 62-64 goal (float32 values, jsbsim_gym.py:321-323)             */
+  F16C_LAST_D = 65,  /* PositionReward.last_distance (float32)                         */
+  F16C_STEP = 66,    /* JSBSimEnv.current_step                                          */
+  F16C_EP_RET = 67,  /* Monitor episode return (sum of float64 rewards)                */
+  F16C_EP_COUNT = 68,/* resets so far (keys the device goal RNG)                        */
+  F16C_WIND = 69,    /* 69-71 steady wind NED (fps)                                     */
+  F16C_N = 72
+};
+enum f16_latch_index {
+  F16L_ALPHA = 0, F16L_BETA, F16L_MACH, F16L_VC_KTS, F16L_VG_FPS,
+  F16L_P_AERO, F16L_Q_AERO, F16L_R_AERO, F16L_NPY, F16L_NPZ, F16L_N
+};
+
+/* flags */
+#define F16_FLAG_NO_AUTORESET 0x1 /* leave done lanes un-reset (caller resets)          */
+
+typedef struct f16env_config {
+  int32_t n_envs;       /* envs on this device                                          */
+  int32_t stack_k;      /* frames per observation (reference NUM_STACKED_FRAMES=10 :58)  */
+  int32_t down_sample;  /* FDM frames per env step (reference 4, :157)                   */
+  int32_t max_steps;    /* truncation (reference 1200, :159 and TimeLimit :541)          */
+  int32_t flags;
+  int32_t reserved0;
+  double dt;            /* FDM frame (JSBSim default 1/120 s)                           */
+  double dg_m;          /* goal cylinder radius (reference 100 m, :163)                  */
+  double goal_gain;     /* PositionReward gain (reference 1e-2, :532)                    */
+  double crash_alt_m;   /* crash altitude (reference 10 m, :245)                         */
+  uint64_t seed;        /* device RNG seed for auto-reset goals                          */
+  int64_t env_id_base;  /* global id of local env 0 (multi-GPU shards key the RNG by it) */
+  double ic[F16_IC_N];  /* default initial condition                                    */
+} f16env_config;
+
+typedef struct f16env* f16env_t;
+
+/* Fill *cfg with the reference's defaults (n_envs=1, K=10, down_sample=4, ...). */
+int f16env_config_default(f16env_config* cfg);
+
+/* Create a handle on `device`; allocates the SoA state (no per-step allocation later). */
+int f16env_create(const f16env_config* cfg, int device, f16env_t* out);
+int f16env_destroy(f16env_t h);
+
+/* Bytes of device state held by the handle / persistent bytes per env (roofline S). */
+size_t f16env_state_bytes(f16env_t h);
+int f16env_state_bytes_per_env(void);
+
+/* Reset the lanes where mask[i] != 0 (mask NULL = all).
+ *   goals: N x 3 float (x, y, alt in m) or NULL -> device Philox goal RNG
+ *   ic:    N x F16_IC_N double or NULL -> the config's default IC (template copy)
+ *   obs:   N x K x 15 float; rows of reset lanes are written (K copies of frame 0). */
+int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goals,
+                 const double* ic, float* obs);
+
+/* One env step for all N lanes.
+ *   act          N x 4 float (aileron, elevator, rudder, throttle cmd; NOT clipped,
+ *                as jsbsim_gym.py:216-222)
+ *   obs_prev     N x K x 15 float, the previous observation (may equal obs)
+ *   obs          N x K x 15 float output (reset obs for lanes that finished)
+ *   rew          N float; terminated / truncated N uint8
+ *   terminal_obs N x K x 15 float; only rows of finished lanes are written (may be NULL)
+ *   ep_return    N double; ep_len N int32: valid where the lane finished (may be NULL)
+ *   done_idx     N int32 + n_done (1 int32): compacted list of finished lanes, unordered
+ *                (may be NULL; n_done must be zeroed by the callee -- it is) */
+int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_prev, float* obs,
+                float* rew, uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
+                double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done);
+
+/* Canonical state export/import: canon is N x F16C_N double (device). */
+int f16env_get_state(f16env_t h, void* stream, double* canon);
+int f16env_set_state(f16env_t h, void* stream, const double* canon);
+
+/* Trim each lane for steady wings-level flight at ic[F16_IC_H_SL_FT], ic[F16_IC_U_FPS]
+ * (interpreted as true airspeed, fps) and write the resulting IC (alpha folded into
+ * theta/u/w, trim commands in F16_IC_CMD_*) to ic_out (N x F16_IC_N double, device).
+ * residual_out (N x 3 double, may be NULL): |udot|, |wdot|, |qdot| after the solve. */
+int f16env_trim(f16env_t h, void* stream, const double* ic_in, double* ic_out,
+                double* residual_out);
+
+/* Uniform actions over the Box [-1,-1,-1,0]..[1,1,1,1] from Philox4x32-10 keyed by
+ * (seed; global env id, step). act: N x 4 float. */
+int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step, float* act);
+
+/* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
+ * HBM bytes one env-step moves. */
+const char* f16env_step_kernel_name(void);
+double f16env_algorithmic_bytes_per_env_step(int stack_k);
+
+const char* f16env_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* F16ENV_H */

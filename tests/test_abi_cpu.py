@@ -1,0 +1,108 @@
+"""CPU checks of the drop-in boundary: the C-ABI library builds, loads and exports every
+entry point include/f16env.h declares; the Python mirror matches the header; the product
+package never reaches into oracle/ (no CPU fallback)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "f16env.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(f16env_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def so_path():
+    from f16_jsb_amd.build import build
+    return build()
+
+
+def test_library_exports_every_declared_symbol(so_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", so_path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (f16env_\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_without_gpu(so_path):
+    from f16_jsb_amd import _lib
+    L = _lib.lib()  # imports torch first, then dlopens libf16env.so
+    for name in declared_functions():
+        assert hasattr(L, name)
+    assert set(_lib.EXPORTED_SYMBOLS) == set(declared_functions())
+    # pure functions need no device
+    assert L.f16env_step_kernel_name() == b"f16_step_kernel"
+    s = L.f16env_state_bytes_per_env()
+    assert 200 <= s <= 400
+    assert L.f16env_algorithmic_bytes_per_env_step(4) == 16 + 60 * 4 + 60 * 3 + 4 + 2 + 2 * s
+
+
+def test_config_default_matches_python_mirror(so_path):
+    from f16_jsb_amd import _lib
+    from f16_jsb_amd.abi import EnvConfig, config_default
+    c = EnvConfig()
+    assert _lib.lib().f16env_config_default(ctypes.byref(c)) == 0
+    p = config_default()
+    for f, _ in EnvConfig._fields_:
+        a, b = getattr(c, f), getattr(p, f)
+        if f == "ic":
+            assert list(a) == list(b)
+        else:
+            assert a == b, f
+
+
+def test_header_enums_match_python_mirror():
+    from f16_jsb_amd import abi
+    src = open(HDR).read()
+    for name, val in re.findall(r"\b(F16C_\w+)\s*=\s*(\d+)", src):
+        assert getattr(abi, name) == int(val), name
+    ic_names = re.findall(r"\b(F16_IC_\w+)\s*[,=]", src)
+    for i, name in enumerate(n for n in ic_names if n != "F16_IC_LAT_GEOD_RAD" or True):
+        pass
+    assert abi.F16_IC_N == 19 and abi.F16C_N == 72
+    assert "#define F16_OBS_DIM 15" in src
+
+
+def test_create_without_gpu_fails_loudly(so_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd._lib import F16EnvError
+    with pytest.raises(F16EnvError):
+        F16Envs(4)
+
+
+def test_product_never_imports_oracle(so_path):
+    """No code path of the product reaches the oracle: no Python import of it, no #include
+    of oracle/ sources, and libf16env.so does not link it."""
+    pkg = os.path.join(ROOT, "f16_jsb_amd")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            txt = open(os.path.join(dp, f), errors="ignore").read() if f.endswith((".py", ".hip", ".h")) else ""
+            assert not re.search(r"^\s*(import|from)\s+\S*oracle", txt, re.M), f
+            assert not re.search(r"#include\s+\S*oracle", txt), f
+            assert "f16ref_" not in txt, f
+    needed = subprocess.run(["readelf", "-d", so_path], capture_output=True, text=True).stdout
+    assert "f16ref" not in needed
+
+
+def test_spaces_match_reference_bounds():
+    from f16_jsb_amd import spaces
+    obs = spaces.observation_space(10)
+    assert obs.shape == (10, 15) and obs.dtype == np.float32
+    assert obs.low[0, 3] == 0 and obs.high[0, 4] == np.float32(np.pi + 1e-5)
+    assert obs.low[0, 10] == np.float32(-np.pi / 2 - 1e-5)
+    act = spaces.action_space()
+    np.testing.assert_array_equal(act.low, [-1, -1, -1, 0])
+    np.testing.assert_array_equal(act.high, [1, 1, 1, 1])
