@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the MI355X F-16 environment (BASELINE.json configs[2]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--stack 4]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+A "step" is one VecEnv step (4 FDM frames + obs/reward/termination/auto-reset) of every env
+on the GPU, driven through the device-tensor VecEnv boundary (F16Envs.step) with random
+actions from the device Philox stream, pre-generated into HBM before the timed region.
+Envs shard across ranks (weak scaling, no collective in the stepping loop); the job-level
+value is all ranks' env-steps divided by the max-over-ranks wall time.
+
+Prints ONE JSON line on rank 0 (driver contract), including
+  roofline     -- algorithmic HBM bytes per launch of f16_step_kernel / its average launch
+                  duration (HIP events on the launch stream), vs the 8 TB/s HBM peak;
+                  `traffic` = PMC-measured HBM bytes per launch from profiles/ if present;
+  cpu_baseline -- the CPU oracle (oracle/f16ref.c, fp64 C restatement, OpenMP) timed on this
+                  host on a bounded sample of the same workload (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec at 65 536 envs, 1/2/4/8 MI355X; HBM GB/s fraction"
+HBM_PEAK_GBPS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--stack", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--action-pool", type=int, default=0,
+                    help="distinct pre-generated action batches (0 = one per timed step)")
+    return ap.parse_args()
+
+
+def cpu_baseline(envs, stack, seconds):
+    """Time the fp64 CPU oracle on the same workload (random actions, auto-reset)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    try:
+        from oracle_ref import OracleEnvs, build_oracle, lib
+        build_oracle()
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "unit": "env-steps/s", "cores": 0, "kind": "port",
+                "sample": "oracle unavailable: %s" % e}
+    import numpy as np
+    threads = int(lib().f16ref_threads())
+    n = min(envs, 65536)
+    e = OracleEnvs(n, stack_k=stack, seed=1)
+    e.reset()
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        a = e.sample_actions(1, steps)
+        e.step(a)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 2000:
+            break
+    e.close()
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
+                      "%d envs x %d random-action steps (stack=%d, auto-reset), %d OpenMP threads, %.1f s"
+                      % (n, steps, stack, threads, el)}
+
+
+def load_traffic(envs, stack):
+    """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("envs") == envs and d.get("stack_k") == stack:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from f16_jsb_amd.build import build
+    from f16_jsb_amd.env import F16VecEnv
+
+    if rank == 0 or world == 1:
+        build()
+    if world > 1:
+        dist.barrier()
+
+    n = args.envs
+    venv = F16VecEnv(num_envs=n, stack_k=args.stack, device=dev, seed=args.seed, return_numpy=False,
+                     env_id_base=rank * n)
+    envs = venv.envs
+    venv.reset()
+    pool = args.action_pool if args.action_pool > 0 else args.steps
+    acts = torch.empty((pool, n, 4), dtype=torch.float32, device=dev)
+    for t in range(pool):
+        envs.sample_actions(args.seed + 1000, t, out=acts[t])
+    warm = torch.empty((max(args.warmup, 1), n, 4), dtype=torch.float32, device=dev)
+    for t in range(args.warmup):
+        envs.sample_actions(args.seed + 2000, t, out=warm[t])
+    for t in range(args.warmup):
+        envs.step(warm[t])
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    start_ev, end_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    start_ev.record(stream)
+    for t in range(args.steps):
+        envs.step(acts[t % pool])
+    end_ev.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms_per_step = start_ev.elapsed_time(end_ev) / args.steps
+    # per-launch duration of f16_step_kernel: HIP events around each launch on the launch
+    # stream, over a second pass of the same steps (median; events would perturb the
+    # timed loop above)
+    nk = min(args.steps, 200)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
+    for t in range(nk):
+        ev[t][0].record(stream)
+        envs.step(acts[t % pool])
+        ev[t][1].record(stream)
+    torch.cuda.synchronize()
+    durs = sorted(s.elapsed_time(e) for s, e in ev)
+    kern_ms = durs[len(durs) // 2]
+    done_frac = float(((envs.term | envs.trunc).sum()).item()) / n
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms, gpu_ms_per_step = float(tt[0]), float(tt[1]), float(tt[2])
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    total_env_steps = n * world * args.steps
+    value = total_env_steps / elapsed
+    bytes_per_env_step = envs.algorithmic_bytes_per_env_step()
+    bytes_per_launch = bytes_per_env_step * n
+    # launch duration used for the roofline: GPU time of the timed region / launches (the
+    # region is back-to-back f16_step_kernel launches; includes ~1-2 us dispatch gaps, so it
+    # bounds the rocprof kernel duration from above). The per-launch event median (which also
+    # counts event overhead) is reported beside it.
+    achieved = bytes_per_launch / (gpu_ms_per_step * 1e-3) / 1e9
+    traffic = load_traffic(n, args.stack)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "BASELINE cfg3: %d F-16 envs per MI355X, waypoint-goal task, stack=%d, random actions "
+                        "(device Philox, pre-generated in HBM), auto-reset on done" % (n, args.stack),
+            "envs_per_gpu": n,
+            "global_envs": n * world,
+            "stack_k": args.stack,
+            "fdm_frames_per_step": 4,
+            "parallelism": "env-sharded x%d (no collective in the step loop)" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5),
+            "traffic": traffic,
+            "kernel": "f16_step_kernel",
+            "kernel_ms": round(gpu_ms_per_step, 5),
+            "kernel_timing": "HIP events around the timed region on the launch stream / launches",
+            "kernel_ms_event_pair_median": round(kern_ms, 5),
+            "algorithmic_bytes_per_env_step": bytes_per_env_step,
+            "launch_env_steps": n,
+        },
+        "done_fraction_last_step": round(done_frac, 5),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -315,27 +315,54 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
     }
   }
   __syncthreads();
-  // ordered stack rebuild: each wave copies its 64 rows, row by row, coalesced
-  const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
-  for (int rr = 0; rr < 64; ++rr) {
-    const int64_t row = row0 + rr;
-    if (row >= a.E.n) break;
-    const int li = wave * 64 + rr;
-    const bool d = sDone[li] != 0;
-    const float* prev = a.obs_prev + row * KC;
-    float* out = a.obs + row * KC;
-    if (!d) {
-      for (int c = lane; c < KC; c += 64)
-        out[c] = (c < HC) ? prev[c + F16_OBS_DIM] : sF[li * FRAME_PITCH + (c - HC)];
-    } else {
-      float* tout = a.tobs ? a.tobs + row * KC : nullptr;
+  // Ordered stack rebuild. A wave's 64 rows are one contiguous block of 64*K*15 floats in
+  // both obs_prev and obs, and out[j] = prev[j + 15] except in each row's last frame, so the
+  // wave walks the block with flat, coalesced indices j = lane + 64*it (row/col tracked
+  // incrementally, no division). Loads are issued in chunks of 16 before their stores so
+  // the latency overlaps; chunks only ever read ahead of what earlier chunks wrote, which
+  // keeps the in-place mode (obs_prev == obs) correct.
+  {
+    const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
+    const int64_t rows = a.E.n - row0 < 64 ? a.E.n - row0 : 64;
+    if (rows > 0) {
+      const float* prev = a.obs_prev + row0 * KC;
+      float* out = a.obs + row0 * KC;
+      float* tout = a.tobs ? a.tobs + row0 * KC : nullptr;
       const bool autoreset = !(a.E.flags & F16_FLAG_NO_AUTORESET);
-      for (int c = lane; c < KC; c += 64) {
-        const float v = (c < HC) ? prev[c + F16_OBS_DIM] : sF[li * FRAME_PITCH + (c - HC)];
-        if (tout) tout[c] = v;
-        out[c] = autoreset ? sR[li * FRAME_PITCH + (c % F16_OBS_DIM)] : v;
+      const int total = (int)rows * KC;
+      int row = lane / KC, col = lane - (lane / KC) * KC;  // one division, at start
+      constexpr int CH = 16;
+      for (int base = 0; base < total; base += 64 * CH) {
+        float v[CH];
+        int rw[CH], cl[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int j = base + 64 * u + lane;
+          rw[u] = row; cl[u] = col;
+          float x = 0.0f;
+          if (j < total) {
+            const int li = wave * 64 + row;
+            x = (col < HC) ? prev[j + F16_OBS_DIM] : sF[li * FRAME_PITCH + (col - HC)];
+          }
+          v[u] = x;
+          col += 64;
+          while (col >= KC) { col -= KC; ++row; }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int j = base + 64 * u + lane;
+          if (j < total) {
+            const int li = wave * 64 + rw[u];
+            if (!sDone[li]) {
+              out[j] = v[u];
+            } else {
+              if (tout) tout[j] = v[u];
+              out[j] = autoreset ? sR[li * FRAME_PITCH + (cl[u] % F16_OBS_DIM)] : v[u];
+            }
+          }
+        }
       }
     }
   }

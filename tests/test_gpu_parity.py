@@ -1,0 +1,303 @@
+"""HIP path (fp32 kernel, fp64 ECI position) vs the CPU oracle (fp64), through the C ABI.
+
+Tolerances (calibrated from tests/parity_report.py on MI355X, with >= 10x margin):
+  * IC / one env step from an identical injected state: fp32 round-off level
+      positions 1e-3 m, angles / alpha / beta 5e-6 rad, mach 5e-6, body rates 5e-5 rad/s;
+  * constant-action trajectories (non-chaotic), 300 steps = 10 s:
+      positions 0.05 m, angles 1e-4 rad, mach 1e-5, rates 5e-5 rad/s;
+  * random-action trajectories diverge chaotically: checked to 30 steps
+      (1 s) at positions 5e-3 m, angles 5e-5 rad, rates 5e-4 rad/s; beyond that only the
+      divergence report (parity_report.py) is produced;
+  * integer / RNG / env-logic outputs (actions, goals, done flags, step counters,
+      compacted done list) are bit-exact.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle_ref import OracleEnvs, default_ic  # noqa: E402
+from parity_tools import frame_err  # noqa: E402
+
+# per frame component atol: lat*R lon*R h mach alpha beta p q r phi theta psi goal(3)
+TOL_STEP = np.array([1e-3, 1e-3, 1e-3, 5e-6, 5e-6, 5e-6, 5e-5, 5e-5, 5e-5, 5e-6, 5e-6, 5e-6, 0, 0, 0])
+TOL_CONST300 = np.array([5e-2, 5e-2, 5e-2, 1e-5, 1e-5, 1e-5, 5e-5, 5e-5, 5e-5, 1e-4, 1e-4, 1e-4, 0, 0, 0])
+TOL_RAND30 = np.array([5e-3, 5e-3, 5e-3, 2e-5, 5e-5, 5e-5, 5e-4, 5e-4, 5e-4, 5e-5, 5e-5, 5e-5, 0, 0, 0])
+
+
+def _assert_frames(gpu, ref, tol, what):
+    err = frame_err(gpu, ref)
+    bad = err > tol
+    if bad.any():
+        idx = np.argwhere(bad)[0]
+        raise AssertionError("%s: component %d err %.3e > tol %.1e (gpu %r ref %r)" % (
+            what, idx[-1], err[tuple(idx)], tol[idx[-1]], gpu[tuple(idx[:-1])], ref[tuple(idx[:-1])]))
+
+
+def _random_ics(n, rng):
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = rng.uniform(3000, 30000, n)          # h ft
+    ic[:, 3] = rng.uniform(600, 1200, n)            # u fps
+    ic[:, 6] = rng.uniform(-0.17, 0.17, n)          # phi
+    ic[:, 7] = rng.uniform(-0.17, 0.17, n)          # theta
+    ic[:, 8] = rng.uniform(0, 2 * np.pi, n)         # psi
+    ic[:, 9:12] = rng.uniform(-0.05, 0.05, (n, 3))  # p q r
+    ic[:, 15] = rng.uniform(0.0, 1.0, n)            # throttle cmd at IC
+    return ic
+
+
+@pytest.fixture(scope="module")
+def torch_mod(gpu):
+    import torch
+    return torch
+
+
+def _pair(n, k, **kw):
+    from f16_jsb_amd.env import F16Envs
+    return OracleEnvs(n, stack_k=k, **kw), F16Envs(n, stack_k=k, **kw)
+
+
+def test_ic_parity_random_ics(torch_mod):
+    n = 128
+    rng = np.random.default_rng(0)
+    ic = _random_ics(n, rng)
+    goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
+    ref, g = _pair(n, 4, seed=1)
+    o_r = ref.reset(goals=goals, ic=ic)
+    o_g = g.reset(goals=goals, ic=ic).cpu().numpy()
+    _assert_frames(o_g[:, -1], o_r[:, -1], TOL_STEP, "IC frame")
+    assert np.all(o_g == o_g[:, :1])
+
+
+def test_one_step_parity_from_identical_states(torch_mod):
+    torch = torch_mod
+    n = 128
+    rng = np.random.default_rng(1)
+    goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
+    ref, g = _pair(n, 4, seed=3)
+    obs = ref.reset(goals=goals, ic=_random_ics(n, rng))
+    g.reset(goals=goals)
+    checked = 0
+    for t in range(120):
+        a = ref.sample_actions(5, t)
+        if t % 15 == 14:
+            g.set_state(ref.get_state())
+            g.set_obs(torch.as_tensor(obs))
+            o_r, r_r, te_r, tr_r, *_ = ref.step(a)
+            out = g.step(torch.as_tensor(a).cuda())
+            alive = ~(te_r | tr_r)
+            _assert_frames(out.obs.cpu().numpy()[alive, -1], o_r[alive, -1], TOL_STEP, "one step @%d" % t)
+            np.testing.assert_allclose(out.rew.cpu().numpy()[alive], r_r[alive], atol=1e-4)
+            checked += int(alive.sum())
+            obs = o_r
+        else:
+            obs = ref.step(a)[0]
+    assert checked > 200
+
+
+def test_constant_action_trajectory(torch_mod):
+    torch = torch_mod
+    n = 32
+    rng = np.random.default_rng(2)
+    goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
+    ref, g = _pair(n, 4, seed=4)
+    ref.reset(goals=goals)
+    g.reset(goals=goals)
+    act = np.tile(np.array([[0.05, -0.1, 0.02, 0.7]], np.float32), (n, 1))
+    act[:, 3] = np.linspace(0.2, 1.0, n)
+    ta = torch.as_tensor(act).cuda()
+    for t in range(300):
+        o_r, r_r, te_r, tr_r, *_ = ref.step(act)
+        out = g.step(ta)
+        np.testing.assert_array_equal(out.terminated.cpu().numpy().astype(bool), te_r)
+    _assert_frames(out.obs.cpu().numpy()[:, -1], o_r[:, -1], TOL_CONST300, "constant action @300")
+
+
+def test_random_action_short_horizon(torch_mod):
+    n = 256
+    rng = np.random.default_rng(3)
+    goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
+    ref, g = _pair(n, 4, seed=5)
+    ref.reset(goals=goals)
+    g.reset(goals=goals)
+    for t in range(1, 31):
+        a = ref.sample_actions(99, t)
+        o_r, r_r, te_r, tr_r, _, _, _ = ref.step(a)
+        out = g.step(g.sample_actions(99, t))
+        np.testing.assert_array_equal(out.terminated.cpu().numpy().astype(bool), te_r)
+        np.testing.assert_array_equal(out.truncated.cpu().numpy().astype(bool), tr_r)
+        np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3)
+    _assert_frames(out.obs.cpu().numpy()[:, -1], o_r[:, -1], TOL_RAND30, "random actions @30")
+
+
+def test_sample_actions_bitexact(torch_mod):
+    n = 1000
+    ref, g = _pair(n, 1, env_id_base=12345)
+    for step in (0, 1, 7, 2**33 + 5):
+        np.testing.assert_array_equal(g.sample_actions(42, step).cpu().numpy(), ref.sample_actions(42, step))
+    a = g.sample_actions(42, 3).cpu().numpy()
+    assert a[:, :3].min() >= -1 and a.max() < 1 and a[:, 3].min() >= 0
+
+
+def test_autoreset_crash_parity(torch_mod):
+    """Diving lanes crash (-10, jsbsim_gym.py:245-247), auto-reset (dummy_vec_env.py:68-71):
+    terminal obs, Monitor return/length, Philox goals of the new episode are bit-exact."""
+    torch = torch_mod
+    n = 64
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(150.0, 600.0, n)   # ft
+    ic[:, 7] = -0.6                           # steep dive
+    goals = np.tile(np.array([[3000.0, 3000.0, 2000.0]], np.float32), (n, 1))
+    ref, g = _pair(n, 4, seed=77)
+    ref.reset(goals=goals, ic=ic)
+    g.reset(goals=goals, ic=ic)
+    act = np.zeros((n, 4), np.float32)
+    ta = torch.as_tensor(act).cuda()
+    saw = np.zeros(n, bool)
+    for t in range(40):
+        o_r, r_r, te_r, tr_r, tobs_r, eret_r, elen_r = ref.step(act)
+        out = g.step(ta)
+        te_g = out.terminated.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(te_g, te_r)
+        if te_r.any():
+            d = te_r
+            saw |= d
+            np.testing.assert_allclose(out.rew.cpu().numpy()[d], r_r[d], atol=2e-3)
+            np.testing.assert_allclose(out.ep_return.cpu().numpy()[d], eret_r[d], atol=1e-3)
+            np.testing.assert_array_equal(out.ep_len.cpu().numpy()[d], elen_r[d])
+            _assert_frames(out.terminal_obs.cpu().numpy()[d, -1], tobs_r[d, -1], TOL_CONST300, "terminal obs")
+            og = out.obs.cpu().numpy()[d]
+            # new episode: K copies of the IC frame, goal from the device Philox stream (bit-exact)
+            np.testing.assert_array_equal(og[:, :, 12:], o_r[d][:, :, 12:])
+            _assert_frames(og[:, -1], o_r[d][:, -1], TOL_STEP, "reset frame")
+    assert saw.all()
+
+
+def test_trim_parity_and_level_flight(torch_mod):
+    torch = torch_mod
+    n = 16
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(3000, 30000, n)
+    ic[:, 3] = np.linspace(700, 1100, n)
+    ref, g = _pair(n, 1, seed=0)
+    t_r, res_r = ref.trim(ic)
+    t_g, res_g = g.trim(ic)
+    t_g, res_g = t_g.cpu().numpy(), res_g.cpu().numpy()
+    assert np.all(res_r < 1e-3)
+    assert np.all(res_g < 2e-2), res_g
+    np.testing.assert_allclose(t_g[:, 7], t_r[:, 7], atol=2e-4)     # alpha = theta
+    np.testing.assert_allclose(t_g[:, 13], t_r[:, 13], atol=2e-3)   # elevator cmd
+    np.testing.assert_allclose(t_g[:, 15], t_r[:, 15], atol=2e-3)   # throttle cmd
+    # fly the oracle's trim on both paths: smooth, so the tolerance holds over 40 s
+    goals = np.zeros((n, 3), np.float32)
+    o_r = ref.reset(goals=goals, ic=t_r)
+    g.reset(goals=goals, ic=t_r)
+    act = np.zeros((n, 4), np.float32)
+    act[:, 1], act[:, 3] = t_r[:, 13], t_r[:, 15]
+    ta = torch.as_tensor(act).cuda()
+    h0 = o_r[:, 0, 2].copy()
+    for t in range(1199):  # step 1200 truncates and auto-resets
+        o_r, *_ = ref.step(act)
+        out = g.step(ta)
+    o_g = out.obs.cpu().numpy()
+    tol = np.array([2.0, 2.0, 0.5, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-3, 1e-4, 1e-3, 0, 0, 0])
+    _assert_frames(o_g[:, -1], o_r[:, -1], tol, "trimmed flight @1199")
+    assert np.all(np.abs(o_r[:, -1, 2] - h0) < 60.0)
+
+
+def test_large_batch_properties(torch_mod):
+    """65 536 envs (BASELINE cfg3 shape), 200 random-action steps: finite outputs, the
+    ordered-stack invariant obs[t][:, :-1] == obs[t-1][:, 1:] on continuing lanes
+    (bit-exact), auto-reset rows are K copies, determinism across handles, and the
+    in-place (obs_prev == obs) ABI mode equals the ping-pong mode bit for bit."""
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd._lib import lib
+    n, k = 65536, 4
+    a = F16Envs(n, stack_k=k, seed=9)
+    b = F16Envs(n, stack_k=k, seed=9)
+    a.reset()
+    b.reset()
+    prev = a.obs.clone()
+    inplace = b.obs  # b steps in place through the raw ABI
+    L = lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n_done_total = 0
+    for t in range(200):
+        act = a.sample_actions(3, t)
+        out = a.step(act)
+        rc = L.f16env_step(b._h, stream, act.data_ptr(), inplace.data_ptr(), inplace.data_ptr(), b.rew.data_ptr(),
+                           b.term.data_ptr(), b.trunc.data_ptr(), b.terminal_obs.data_ptr(), b.ep_return.data_ptr(),
+                           b.ep_len.data_ptr(), None, None)
+        assert rc == 0
+        done = (out.terminated | out.truncated).bool()
+        n_done_total += int(done.sum())
+        assert torch.isfinite(out.obs).all()
+        assert torch.equal(out.obs, inplace)
+        assert torch.equal(out.rew, b.rew)
+        cont = ~done
+        assert torch.equal(out.obs[cont, :-1], prev[cont, 1:])
+        if done.any():
+            assert torch.equal(out.terminal_obs[done, :-1], prev[done, 1:])
+            r = out.obs[done]
+            assert torch.equal(r, r[:, :1].expand_as(r))
+        prev = out.obs.clone()
+    assert n_done_total > 0
+
+
+def test_done_index_compaction(torch_mod):
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd._lib import lib
+    n = 5000
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(100.0, 3000.0, n)
+    ic[:, 7] = -0.8
+    e = F16Envs(n, stack_k=2, seed=1)
+    e.reset(ic=ic)
+    idx = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    L = lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    act = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    seen = 0
+    for t in range(20):
+        nxt = e._obs[e._cur ^ 1]
+        rc = L.f16env_step(e._h, stream, act.data_ptr(), e.obs.data_ptr(), nxt.data_ptr(), e.rew.data_ptr(),
+                           e.term.data_ptr(), e.trunc.data_ptr(), e.terminal_obs.data_ptr(), e.ep_return.data_ptr(),
+                           e.ep_len.data_ptr(), idx.data_ptr(), cnt.data_ptr())
+        assert rc == 0
+        e._cur ^= 1
+        want = torch.nonzero((e.term | e.trunc).bool()).flatten().cpu().numpy()
+        got = np.sort(idx[: int(cnt.item())].cpu().numpy())
+        np.testing.assert_array_equal(got, want)
+        seen += len(want)
+    assert seen > 0
+
+
+def test_vecenv_sb3_contract(torch_mod):
+    from f16_jsb_amd import F16VecEnv, reference_goal
+    n = 8
+    env = F16VecEnv(num_envs=n, stack_k=10, seed=0)
+    assert env.observation_space.shape == (10, 15) and env.action_space.shape == (4,)
+    seeds = env.seed(100)
+    obs = env.reset()
+    assert isinstance(obs, np.ndarray) and obs.shape == (n, 10, 15) and obs.dtype == np.float32
+    for i, s in enumerate(seeds):
+        np.testing.assert_array_equal(obs[i, 0, 12:], reference_goal(s))
+    total = 0
+    for t in range(1300):
+        obs, rew, dones, infos = env.step(np.tile(np.array([[0, -0.2, 0, 0.8]], np.float32), (n, 1)))
+        assert obs.shape == (n, 10, 15) and rew.dtype == np.float32 and dones.dtype == bool
+        assert len(infos) == n and all("TimeLimit.truncated" in i for i in infos)
+        for i in np.flatnonzero(dones):
+            assert infos[i]["terminal_observation"].shape == (10, 15)
+            ep = infos[i]["episode"]
+            assert set(ep) == {"r", "l", "t"} and ep["l"] <= 1200
+            total += 1
+    assert total >= n  # every lane finished at least once (crash / goal / 1200-step truncation)
+    env.close()

@@ -1,0 +1,47 @@
+#!/usr/bin/env bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Each step has its own time limit; a step that faults / aborts / times out ends the session
+# (pytest's "tests failed" exit 1 does not). Output lands in gpurun_out/.
+#   usage: tools/gpu_session.sh [tag] [steps...]   steps: tests smoke bench prof pmc report
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"tests smoke bench prof"}
+OUT=gpurun_out
+mkdir -p "$OUT"
+
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 lim=$2
+  shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[session] $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "[session] stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+  return 0
+}
+
+python -c "from f16_jsb_amd.build import build; build()" || exit 3
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -x ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 1000 --warmup 50 ;;
+    report) run parity_report 600 python tests/parity_report.py --n 256 --steps 300 --json "$OUT/parity_$TAG.json" ;;
+    prof)
+      run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \
+        python bench.py --steps 300 --warmup 20 --no-cpu-baseline ;;
+    pmc)
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- \
+        python bench.py --steps 50 --warmup 5 --no-cpu-baseline
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o run --output-format csv -- \
+        python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+  esac
+done
+echo "[session] done"
