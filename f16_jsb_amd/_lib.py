@@ -12,7 +12,7 @@ import os
 
 from .abi import EnvConfig
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libf16env.so")
+LIB_PATH = os.environ.get("F16ENV_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libf16env.so")
 
 _lib = None
 

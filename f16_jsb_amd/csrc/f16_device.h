@@ -18,6 +18,41 @@
 
 namespace f16 {
 
+// Diagnostic build only (-DF16_STAMPS): per-wave cycle totals per code section, from
+// s_memtime (a shader-clock counter), accumulated in scalar registers and stored once per
+// wave by lane 0. The production build compiles every F16_STAMP to nothing.
+enum StampSection {
+  ST_LOAD = 0, ST_PROP, ST_DERIVE, ST_ATM, ST_FCS, ST_AUX, ST_ENGINE, ST_AERO, ST_ACCEL,
+  ST_FRAME_OBS, ST_REWARD, ST_RESET, ST_SYNC, ST_COPY, ST_STORE, ST_N
+};
+#ifdef F16_STAMPS
+struct Stamps {
+  unsigned long long acc[ST_N];
+  unsigned long long last;
+};
+__device__ __forceinline__ unsigned long long memtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define F16_STAMP(S, sec)                    \
+  do {                                       \
+    const unsigned long long t_ = memtime(); \
+    (S).acc[sec] += t_ - (S).last;           \
+    (S).last = t_;                           \
+  } while (0)
+#define F16_STAMP_ARG , Stamps& stamps
+#define F16_STAMP_PASS , stamps
+#else
+#define F16_STAMP(S, sec) \
+  do {                    \
+  } while (0)
+#define F16_STAMP_ARG
+#define F16_STAMP_PASS
+#endif
+
 // ------------------------------------------------------------------------------------------
 // constants shared with the host (filled by f16env_create from the same formulas as the
 // oracle's init_consts(), in double, then stored in the kernel argument block)
@@ -28,6 +63,7 @@ struct ModelConsts {
   float rp[3], eye[3], eng[3];  // AERORP / EYEPOINT / thruster rel. CG (body ft)
   float inv_gref;            // 1 / (GM/a^2)
   float rho_sl, a_sl, p_sl;  // US-76 sea level (slug/ft3, ft/s, psf)
+  float inv_rho_sl, inv_p_sl;
   float kts_per_fps;
   double cos_dE, sin_dE;     // rotation of the Earth per frame (omega * dt)
   double dt;
@@ -174,42 +210,38 @@ struct Seg {  // bracketing segment i-1..i and clamped factor
   int i;
   float f;
 };
-// 2-D style bracket (FGTable::GetValue(row, col)): i in [1, n-1], factor clamped to [0,1].
+__device__ __forceinline__ float rcpf(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+
+// FGTable::GetValue bracket: i = 1 + #{k in 1..N-2 : bp[k] < x} (literal compares), then the
+// segment's (lo, 1/span) pair from LDS; factor clamped to [0, 1] (2-D semantics, and the
+// 1-D end clamps coincide with it).
 template <int N>
-__device__ __forceinline__ Seg bracket(const float (&bp)[N], float x) {
+__device__ __forceinline__ Seg bracket(const float (&bp)[N], const float* pairs, float x) {
   int i = 1;
 #pragma unroll
   for (int k = 1; k < N - 1; ++k) i += (bp[k] < x) ? 1 : 0;
-  float lo = bp[0], hi = bp[1];
-#pragma unroll
-  for (int k = 2; k < N; ++k) {
-    lo = (i == k) ? bp[k - 1] : lo;
-    hi = (i == k) ? bp[k] : hi;
-  }
-  float f = (x - lo) / (hi - lo);
+  const float2 p = reinterpret_cast<const float2*>(pairs)[i - 1];
+  float f = (x - p.x) * p.y;
+  f = fminf(fmaxf(f, 0.0f), 1.0f);
+  return {i, f};
+}
+// uniform grid x0 + k*h (k = 0..N-1): same bracket semantics without a search
+__device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, int n) {
+  const float u = (x - x0) * inv_h;
+  int i = (int)floorf(u) + 1;
+  i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
+  float f = u - (float)(i - 1);
   f = fminf(fmaxf(f, 0.0f), 1.0f);
   return {i, f};
 }
 __device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (b - a) + a; }
 
-// 1-D lookup over an LDS value array with literal breakpoints (FGTable::GetValue(key))
+// 1-D lookup over LDS values with literal breakpoints and LDS (lo, 1/span) pairs
 template <int N>
-__device__ __forceinline__ float tab1(const float (&bp)[N], const float* v, float x) {
-  if (x <= bp[0]) return v[0];
-  if (x >= bp[N - 1]) return v[N - 1];
-  Seg s = bracket(bp, x);
+__device__ __forceinline__ float tab1(const float (&bp)[N], const float* pairs, const float* v, float x) {
+  const Seg s = bracket(bp, pairs, x);
   return lerp1(s.f, v[s.i - 1], v[s.i]);
-}
-// 2-D lookup, row-major [nr][nc] LDS values
-template <int NR, int NC>
-__device__ __forceinline__ float tab2(const float (&rb)[NR], const float (&cb)[NC], const float* v,
-                                      float x, float y) {
-  Seg r = bracket(rb, x), c = bracket(cb, y);
-  float a0 = v[(r.i - 1) * NC + c.i - 1], a1 = v[r.i * NC + c.i - 1];
-  float b0 = v[(r.i - 1) * NC + c.i], b1 = v[r.i * NC + c.i];
-  float c1 = lerp1(r.f, a0, a1);
-  float c2 = lerp1(r.f, b0, b1);
-  return c1 + c.f * (c2 - c1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -229,24 +261,25 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   constexpr float GMR = 9.80665f * 0.0289644f / 8.31432f;
   constexpr float R = 8.31432f / 0.0289644f;
   const float z = h_ft * 0.3048f;
-  const float H = 6356766.0f * z / (6356766.0f + z);
+  const float H = 6356766.0f * z * rcpf(6356766.0f + z);
   int b = 0;
 #pragma unroll
   for (int k = 1; k < 7; ++k) b += (H >= Hb[k]) ? 1 : 0;
-  float hb = Hb[0], lb = Lb[0], tb = Tb[0], pb = Pb[0];
+  constexpr float EX[7] = {GMR / Lb[0], 0.0f, GMR / Lb[2], GMR / Lb[3], 0.0f, GMR / Lb[5], GMR / Lb[6]};
+  float hb = Hb[0], lb = Lb[0], tb = Tb[0], pb = Pb[0], ex = EX[0];
 #pragma unroll
   for (int k = 1; k < 7; ++k) {
-    if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; }
+    if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; ex = EX[k]; }
   }
   float T, P;
   if (lb != 0.0f) {
     T = tb + lb * (H - hb);
-    P = pb * __powf(tb / T, GMR / lb);
+    P = pb * __powf(tb * rcpf(T), ex);
   } else {
     T = tb;
-    P = pb * __expf(-GMR * (H - hb) / tb);
+    P = pb * __expf(-GMR * (H - hb) * rcpf(tb));
   }
-  const float rho = P / (R * T);
+  const float rho = P * rcpf(R * T);
   Atm o;
   o.T = T * 1.8f;
   o.P = P * (1.0f / 47.88025898033584f);
@@ -264,14 +297,14 @@ __device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts
     pt = p * (x * x * x * sqrtf(x));
   } else {
     float m2 = mach * mach, d = 7.0f * m2 - 1.0f;
-    pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) / (d * d * sqrtf(d));
+    pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * sqrtf(d));
   }
   const float qc = pt - p;
-  const float A = qc / C.p_sl + 1.0f;
+  const float A = qc * C.inv_p_sl + 1.0f;
   float M = sqrtf(5.0f * (__powf(A, 1.0f / 3.5f) - 1.0f));
   if (M > 1.0f) {
     for (int i = 0; i < 10; ++i) {
-      float t = 1.0f - 1.0f / (7.0f * M * M);
+      float t = 1.0f - rcpf(7.0f * M * M);
       M = 0.8812848543473311f * sqrtf(A * (t * t * sqrtf(t)));
     }
   }
@@ -352,19 +385,21 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, Deri
   const double yE = -se * L.rI[0] + ce * L.rI[1];
   const double zE = L.rI[2];
   const double rxy = sqrt(xE * xE + yE * yE);
-  const double r = sqrt(rxy * rxy + zE * zE);
-  const double inv_r = 1.0 / r;
-  const float slat = (float)(zE * inv_r), clat = (float)(rxy * inv_r);
+  d.h_ft = geodetic_altitude(xE, yE, zE, rxy);
+  // direction cosines only need fp32
+  const float xf = (float)xE, yf = (float)yE, zf = (float)zE, rxyf = (float)rxy;
+  const float rf = sqrtf(rxyf * rxyf + zf * zf);
+  const float inv_r = rcpf(rf);
+  const float slat = zf * inv_r, clat = rxyf * inv_r;
   float slon = 0.0f, clon = 1.0f;
   if (rxy != 0.0) {
-    const double inv = 1.0 / rxy;
-    slon = (float)(yE * inv);
-    clon = (float)(xE * inv);
+    const float inv = rcpf(rxyf);
+    slon = yf * inv;
+    clon = xf * inv;
   }
-  d.h_ft = geodetic_altitude(xE, yE, zE, rxy);
   if (lat_gc_out) {
-    *lat_gc_out = (float)atan2(zE, rxy);
-    *lon_out = (rxy == 0.0) ? 0.0f : (float)atan2(yE, xE);
+    *lat_gc_out = atan2f(zf, rxyf);
+    *lon_out = (rxy == 0.0) ? 0.0f : atan2f(yf, xf);
   }
   // Tec2l (geocentric, FGLocation)
   const float L0 = -clon * slat, L1 = -slon * slat, L2 = clat;
@@ -399,16 +434,14 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, Deri
   d.pqr[2] = L.wI[2] - d.Ti2b[8] * we;
   mtvec(d.Tl2b, d.uvw, d.vned);
   // J2 gravity (FGInertial::GetGravityJ2), ECEF
-  const float rf = (float)r;
-  const float adivr = (float)(WGS_A * inv_r);
+  const float adivr = (float)WGS_A * inv_r;
   const float pre = 1.5f * (float)J2_E * adivr * adivr;
-  const float gm = (float)(GM_E * inv_r * inv_r);
+  const float gm = (float)GM_E * inv_r * inv_r;
   const float xy = 1.0f - 5.0f * slat * slat, zz = 3.0f - 5.0f * slat * slat;
   const float kxy = -gm * (1.0f + pre * xy);
-  d.gE[0] = kxy * (float)(xE * inv_r);
-  d.gE[1] = kxy * (float)(yE * inv_r);
+  d.gE[0] = kxy * clat * clon;
+  d.gE[1] = kxy * clat * slon;
   d.gE[2] = -gm * (1.0f + pre * zz) * slat;
-  (void)rf;
 }
 
 // Euler angles from Tl2b (FGMatrix33::GetEuler)
@@ -437,7 +470,7 @@ __device__ __forceinline__ float kin2(float out, float in, float d0, float d1, f
   in = clipf(in, d0, d1);
   if (ic) return in;
   if (eq_roundoff(in, out)) return out;
-  const float tdt = fabsf((in - out) / rate);
+  const float tdt = fabsf((in - out) * (1.0f / rate));
   if (dt < tdt) return (out < in) ? out + dt * rate : out - dt * rate;
   return in;
 }
@@ -452,7 +485,7 @@ __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic)
     if (ind == 1) { out = in; break; }  // transition time 0 -> infinite rate
     const float rate = 1.0f / 3.0f, lo = 0.0f, hi = 1.0f;
     const float tin = clipf(in, lo, hi);
-    float tdt = fabsf((tin - out) / rate);
+    float tdt = fabsf((tin - out) * 3.0f);  // / rate, rate = 1/3
     if (dt0 < tdt) {
       tdt = dt0;
       out = (out < in) ? out + tdt * rate : out - tdt * rate;
@@ -465,7 +498,7 @@ __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic)
 }
 __device__ __forceinline__ float pidf(float in, float& itot, float& prev, float trig, float kp,
                                       float ki, float kd, float dt, bool ic) {
-  const float dval = ic ? 0.0f : (in - prev) / dt;
+  const float dval = ic ? 0.0f : (in - prev) * rcpf(dt);
   const float delta = (!ic && fabsf(trig) < 0.000001f) ? in : 0.0f;
   if (trig < 0.0f) itot = 0.0f;
   itot += ki * dt * delta;
@@ -499,7 +532,7 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
   o.da = aero_scale(roll_cmd, 0.375f);
   L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
-  const float asc = L.ail * tab1(BP_fcs_aileron_speed_compensated,
+  const float asc = L.ail * tab1(BP_fcs_aileron_speed_compensated, T + OFF_pair_fcs_aileron_speed_compensated,
                                  T + OFF_fcs_v_aileron_speed_compensated, mach);
   const float lflap = clipf(-L.tef - asc, -1.0f, 1.0f);
   const float rflap = clipf(L.tef - asc, -1.0f, 1.0f);
@@ -507,7 +540,8 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   // Pitch
   const float g_corr = L.lx[F16L_NPZ] - tl2b_33;  // cos(theta)cos(phi) == Tl2b(3,3)
   const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
-  const float ele_sched = ele_lim * tab1(BP_fcs_elevator_scheduler, T + OFF_fcs_v_elevator_scheduler, alpha);
+  const float ele_sched = ele_lim * tab1(BP_fcs_elevator_scheduler, T + OFF_pair_fcs_elevator_scheduler,
+                                         T + OFF_fcs_v_elevator_scheduler, alpha);
   const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
   const float ele_trig = (vc < 5.0f) ? 0.0f : 1.0f;
   const float gpid = clipf(pidf(pitch_err, L.ppi, L.ppp, ele_trig, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
@@ -515,7 +549,8 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
   o.de = aero_scale(L.ele, 0.436f);
   // Yaw
-  const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tab1(BP_fcs_yaw_rate_norm, T + OFF_fcs_v_yaw_rate_norm, vg) +
+  const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tab1(BP_fcs_yaw_rate_norm, T + OFF_pair_fcs_yaw_rate_norm,
+                                                          T + OFF_fcs_v_yaw_rate_norm, vg) +
                         L.lx[F16L_NPY] * 0.25f;
   const float rud_trig = (vc < 10.0f) ? 0.0f : 1.0f;
   const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, rud_trig, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
@@ -553,8 +588,22 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
                                             float sigma, const float* T, float dt, bool ic) {
   float tp = throttle_pos, aug_cmd = 0.0f;
   if (tp > 1.0f) { aug_cmd = tp - 1.0f; tp -= aug_cmd; }
-  const float idle = 17800.0f * tab2(BP_engr_IdleThrust, BP_engc_IdleThrust, T + OFF_eng_v_IdleThrust, mach, h_rho);
-  const float mil = (17800.0f - idle) * tab2(BP_engr_MilThrust, BP_engc_MilThrust, T + OFF_eng_v_MilThrust, mach, h_rho);
+  // IdleThrust / MilThrust / AugThrust on one (mach 0..2.6 step 0.2) x (density-alt
+  // -10000..60000 step 10000) grid, interleaved [14][8][3] (Idle/Mil rows clamped beyond
+  // their last mach row, as FGTable does)
+  const Seg er = bracket_uniform(mach, 0.0f, 5.0f, ENGU_NR);
+  const Seg ec = bracket_uniform(h_rho, -10000.0f, 1e-4f, ENGU_NC);
+  const float* e00 = T + OFF_engu_v + ((er.i - 1) * ENGU_NC + ec.i - 1) * 3;
+  const float* e10 = e00 + ENGU_NC * 3;
+  float ev[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float c1 = lerp1(er.f, e00[k], e10[k]);
+    const float c2 = lerp1(er.f, e00[k + 3], e10[k + 3]);
+    ev[k] = c1 + ec.f * (c2 - c1);
+  }
+  const float idle = 17800.0f * ev[0];
+  const float mil = (17800.0f - idle) * ev[1];
   if (ic) {
     L.n2 = 60.0f + tp * 40.0f;
     L.n1 = 30.0f + tp * 70.0f;
@@ -562,7 +611,7 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   } else {
     const float nn = fminf((L.n2 - 60.0f) * (1.0f / 40.0f) + 0.1f, 1.0f);
     const float u = 1.0f - nn;
-    const float spool = (90.0f / 3.36f) / (1.0f + 3.0f * u * u * u + (1.0f - sigma));
+    const float spool = (90.0f / 3.36f) * rcpf(1.0f + 3.0f * u * u * u + (1.0f - sigma));
     L.n2 = seekf(L.n2, 60.0f + tp * 40.0f, spool, spool * 3.0f, dt);
     L.n1 = seekf(L.n1, 30.0f + tp * 70.0f, spool, spool * 2.4f, dt);
   }
@@ -571,7 +620,7 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   if (!(L.flags & LANE_FLAG_AUG)) thrust *= (1.0f - 0.03f);
   if (aug_cmd > 0.0f) {
     L.flags |= LANE_FLAG_AUG;
-    const float tdiff = 29000.0f * tab2(BP_engr_AugThrust, BP_engc_AugThrust, T + OFF_eng_v_AugThrust, mach, h_rho) - thrust;
+    const float tdiff = 29000.0f * ev[2] - thrust;
     thrust += tdiff * aug_cmd;
   } else {
     L.flags &= ~LANE_FLAG_AUG;
@@ -585,23 +634,17 @@ struct AeroIn {
   float de, da, dr, dlef, flap, dsb;
 };
 __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6) {
-  const Seg sa = bracket(BP_alpha_bp, a.alpha);
+  const Seg sa = bracket(BP_alpha_bp, T + OFF_pair_alpha, a.alpha);
   // 16 alpha 1-D tables, [12][16] interleaved; FGTable 1-D semantics (clamp at the ends)
   float A[F16_N_A1D];
   {
     const float* r0 = T + OFF_alpha1d + (sa.i - 1) * F16_N_A1D;
     const float* r1 = r0 + F16_N_A1D;
-    const bool lo = a.alpha <= BP_alpha_bp[0], hi = a.alpha >= BP_alpha_bp[F16_N_ALPHA - 1];
 #pragma unroll
-    for (int k = 0; k < F16_N_A1D; ++k) {
-      float v = lerp1(sa.f, r0[k], r1[k]);
-      v = lo ? r0[k] : v;
-      v = hi ? r1[k] : v;
-      A[k] = v;
-    }
+    for (int k = 0; k < F16_N_A1D; ++k) A[k] = lerp1(sa.f, r0[k], r1[k]);
   }
   // 2-D alpha x elevator: CDDh, CLDh, CmDh ([12][5][3])
-  const Seg se = bracket(BP_de_bp, a.de);
+  const Seg se = bracket(BP_de_bp, T + OFF_pair_de, a.de);
   float ADE[3];
   {
     const float* p00 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 3;
@@ -613,7 +656,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
       ADE[k] = c1 + se.f * (c2 - c1);
     }
   }
-  const Seg sb13 = bracket(BP_beta13_bp, a.beta);
+  const Seg sb13 = bracket(BP_beta13_bp, T + OFF_pair_beta13, a.beta);
   float AB13[2];
   {
     const float* p00 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 2;
@@ -625,7 +668,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
       AB13[k] = c1 + sb13.f * (c2 - c1);
     }
   }
-  const Seg sb7 = bracket(BP_beta7_bp, a.beta);
+  const Seg sb7 = bracket(BP_beta7_bp, T + OFF_pair_beta7, a.beta);
   float AB7[4];
   {
     const float* p00 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 4;
@@ -637,16 +680,18 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
       AB7[k] = c1 + sb7.f * (c2 - c1);
     }
   }
-  const float m = a.mach;
-  const float CDmach = tab1(BP_mach_CDmach, T + OFF_mach_v_CDmach, m);
-  const float CYb_M = tab1(BP_mach_CYb_M, T + OFF_mach_v_CYb_M, m);
-  const float Clb_M = tab1(BP_mach_Clb_M, T + OFF_mach_v_Clb_M, m);
-  const float Clda_M = tab1(BP_mach_Clda_M, T + OFF_mach_v_Clda_M, m);
-  const float Cldr_M = tab1(BP_mach_Cldr_M, T + OFF_mach_v_Cldr_M, m);
-  const float Cma_M = tab1(BP_mach_Cma_M, T + OFF_mach_v_Cma_M, m);
-  const float Cnb_M = tab1(BP_mach_Cnb_M, T + OFF_mach_v_Cnb_M, m);
-  const float Cnda_M = tab1(BP_mach_Cnda_M, T + OFF_mach_v_Cnda_M, m);
-  const float Cndr_M = tab1(BP_mach_Cndr_M, T + OFF_mach_v_Cndr_M, m);
+  // the nine mach tables on their union breakpoint grid, interleaved [13][9]
+  const Seg sm = bracket(BP_machu, T + OFF_pair_machu, a.mach);
+  float MU[MACHU_NT];
+  {
+    const float* r0 = T + OFF_machu_v + (sm.i - 1) * MACHU_NT;
+    const float* r1 = r0 + MACHU_NT;
+#pragma unroll
+    for (int k = 0; k < MACHU_NT; ++k) MU[k] = lerp1(sm.f, r0[k], r1[k]);
+  }
+  const float CDmach = MU[MU_CDmach], CYb_M = MU[MU_CYb_M], Clb_M = MU[MU_Clb_M];
+  const float Clda_M = MU[MU_Clda_M], Cldr_M = MU[MU_Cldr_M], Cma_M = MU[MU_Cma_M];
+  const float Cnb_M = MU[MU_Cnb_M], Cnda_M = MU[MU_Cnda_M], Cndr_M = MU[MU_Cndr_M];
 
   const float qS = a.qbar * S_W;
   const float qc = a.q * a.ci2vel, pb = a.p * a.bi2vel, rb = a.r * a.bi2vel;
@@ -677,7 +722,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 
 // One FGFDMExec::Run(). ce/se: Earth angle cos/sin at the START of the frame (updated here).
 __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se,
-                                      const float* T, const ModelConsts& C, bool ic) {
+                                      const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
   const float dt = (float)C.dt;
   if (!ic) {
     // -- FGPropagate: integrate with the previous frame's derivatives --
@@ -719,15 +764,19 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     const double s2 = se * C.cos_dE + ce * C.sin_dE;
     ce = c2; se = s2;
   }
+  F16_STAMP(stamps, ST_PROP);
   Derived d;
   derive(L, ce, se, d);
+  F16_STAMP(stamps, ST_DERIVE);
   // -- Atmosphere (standard day: density altitude == altitude) --
   const float h = (float)d.h_ft;
   const Atm atm = atmosphere(h);
-  const float sigma = atm.rho / C.rho_sl;
+  const float sigma = atm.rho * C.inv_rho_sl;
+  F16_STAMP(stamps, ST_ATM);
   // -- Systems --
   FcsOut fc;
   fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, dt, ic, fc);
+  F16_STAMP(stamps, ST_FCS);
   // -- Auxiliary --
   float wb[3];
   mvec(d.Tl2b, L.wind, wb);
@@ -738,12 +787,12 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const float suw = sqrtf(muw);
   const float beta = muw > 0.0f ? atan2f(va, suw) : 0.0f;
   const float qbar = 0.5f * atm.rho * vt * vt;
-  const float mach = vt / atm.a;
+  const float mach = vt * rcpf(atm.a);
   const float vc = vcas_kts(mach, atm.P, C);
   const float vg = sqrtf(d.vned[0] * d.vned[0] + d.vned[1] * d.vned[1]);
   float bi2vel = 0.0f, ci2vel = 0.0f;
   if (vt != 0.0f) {
-    const float inv2v = 0.5f / vt;
+    const float inv2v = 0.5f * rcpf(vt);
     bi2vel = B_W * inv2v;
     ci2vel = CBAR * inv2v;
   }
@@ -760,23 +809,25 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   L.lx[F16L_VC_KTS] = vc; L.lx[F16L_VG_FPS] = vg;
   L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
   L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
+  F16_STAMP(stamps, ST_AUX);
   // -- Propulsion --
   const float thrust = engine_run(L, fc.throttle, mach, h, sigma, T, dt, ic);
+  F16_STAMP(stamps, ST_ENGINE);
   // -- Aerodynamics --
   AeroIn ai;
   ai.qbar = qbar; ai.alpha = alpha; ai.beta = beta; ai.mach = mach;
   ai.p = d.pqr[0]; ai.q = d.pqr[1]; ai.r = d.pqr[2];
   ai.bi2vel = bi2vel; ai.ci2vel = ci2vel;
-  ai.kclge = tab1(BP_kclge, T + OFF_kclge_v, hbmac);
+  ai.kclge = tab1(BP_kclge, T + OFF_pair_kclge, T + OFF_kclge_v, hbmac);
   ai.de = fc.de; ai.da = fc.da; ai.dr = fc.dr; ai.dlef = fc.dlef; ai.flap = fc.flap_mix; ai.dsb = fc.dsb;
   float A6[6];
   aero(ai, T, A6);
   // wind (D, Y, L) -> body, vFw = (-D, Y, -L)
   float ca_ = 1.0f, sa_ = 0.0f, cb_ = 1.0f, sb_ = 0.0f;
   if (muw > 0.0f) {
-    const float iuw = 1.0f / suw;
+    const float iuw = rcpf(suw);
     ca_ = ua * iuw; sa_ = wa * iuw;
-    const float ivt = 1.0f / vt;
+    const float ivt = rcpf(vt);
     cb_ = suw * ivt; sb_ = va * ivt;
   }
   const float fw0 = -A6[0], fw1 = A6[1], fw2 = -A6[2];
@@ -793,6 +844,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F[0] += thrust;
   M[1] += C.eng[2] * thrust;
   M[2] += -C.eng[1] * thrust;
+  F16_STAMP(stamps, ST_AERO);
   // -- Accelerations --
 #pragma unroll
   for (int j = 0; j < 3; ++j) L.ba[j] = F[j] * C.inv_mass;
@@ -806,6 +858,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
 #pragma unroll
   for (int j = 0; j < 3; ++j) rhs[j] = M[j] - wxJw[j];
   mvec(C.Jinv, rhs, L.wId);
+  F16_STAMP(stamps, ST_ACCEL);
 }
 
 }  // namespace f16

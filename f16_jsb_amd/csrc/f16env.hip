@@ -140,8 +140,12 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   const float cmd[4] = {(float)ic[F16_IC_CMD_AIL], (float)ic[F16_IC_CMD_ELE], (float)ic[F16_IC_CMD_RUD],
                         (float)ic[F16_IC_CMD_THR]};
   double ce = 1.0, se = 0.0;
-  frame(L, cmd, ce, se, T, C, true);
-  frame(L, cmd, ce, se, T, C, true);
+#ifdef F16_STAMPS
+  Stamps stamps = {};
+#endif
+  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);  // three passes, as oracle apply_ic()
+  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);
+  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);
   for (int j = 0; j < 3; ++j) { L.dv1[j] = 0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }
 }
 
@@ -242,25 +246,45 @@ struct StepArgs {
   ModelConsts C;
 };
 
+#ifdef F16_STAMPS
+__device__ unsigned long long g_stamps[1 << 14][ST_N];  // per wave (diagnostic build)
+#endif
+
 __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
-  __shared__ float sT[F16_BLOB_FLOATS];
+#ifdef F16_STAMPS
+  Stamps stamps = {};
+  stamps.last = memtime();
+#endif
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   __shared__ float sF[BLOCK * FRAME_PITCH];   // final frame per lane
   __shared__ float sR[BLOCK * FRAME_PITCH];   // reset frame per lane (done lanes)
   __shared__ int sDone[BLOCK];
-  stage_tables(sT);
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = k < a.E.n;
   int done = 0;
-  if (live) {
-    Lane L;
+  Lane L;
+  float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {  // issue the state loads before the table staging so their latencies overlap
     lane_load(a.s, k, L);
-    const float4 av = reinterpret_cast<const float4*>(a.act)[k];
+    av = reinterpret_cast<const float4*>(a.act)[k];
+  }
+  stage_tables(sT);
+  if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
-    double ce = cos(L.epa), se = sin(L.epa);
-    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, sT, a.C, false);  // :225-232
+    double ce, se;
+    if (fabs(L.epa) < 0.01) {  // series, exact in fp64 for |epa| < 0.01 (40 s episodes: 3e-3)
+      const double e2 = L.epa * L.epa;
+      ce = 1.0 - e2 * (0.5 - e2 * (1.0 / 24.0 - e2 * (1.0 / 720.0 - e2 * (1.0 / 40320.0))));
+      se = L.epa * (1.0 - e2 * (1.0 / 6.0 - e2 * (1.0 / 120.0 - e2 * (1.0 / 5040.0 - e2 * (1.0 / 362880.0)))));
+    } else {
+      ce = cos(L.epa);
+      se = sin(L.epa);
+    }
+    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, sT, a.C, false F16_STAMP_PASS);  // :225-232
     float f[F16_OBS_DIM];
     make_frame(L, ce, se, f);                                 // :234
+    F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261) in float32, then PositionReward (:493-507)
     float r32;
     int te = 0, tr;
@@ -281,6 +305,7 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       L.ep_ret += r;                                         // monitor.py:96-99
       r32 = (float)r;
     }
+    F16_STAMP(stamps, ST_REWARD);
     a.rew[k] = r32;
     a.term[k] = (uint8_t)te;
     a.trunc[k] = (uint8_t)tr;
@@ -300,7 +325,9 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
         for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f[j];
       }
     }
+    F16_STAMP(stamps, ST_RESET);
     lane_store(a.s, k, L);
+    F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
   // compaction of finished lanes (wave64 ballot)
@@ -315,6 +342,7 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
     }
   }
   __syncthreads();
+  F16_STAMP(stamps, ST_SYNC);
   // Ordered stack rebuild. A wave's 64 rows are one contiguous block of 64*K*15 floats in
   // both obs_prev and obs, and out[j] = prev[j + 15] except in each row's last frame, so the
   // wave walks the block with flat, coalesced indices j = lane + 64*it (row/col tracked
@@ -366,6 +394,14 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       }
     }
   }
+  F16_STAMP(stamps, ST_COPY);
+#ifdef F16_STAMPS
+  if ((threadIdx.x & 63) == 0) {
+    const int w = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    if (w < (1 << 14))
+      for (int q = 0; q < ST_N; ++q) g_stamps[w][q] = stamps.acc[q];
+  }
+#endif
 }
 
 struct ResetArgs {
@@ -378,7 +414,7 @@ struct ResetArgs {
   ModelConsts C;
 };
 __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
-  __shared__ float sT[F16_BLOB_FLOATS];
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   stage_tables(sT);
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (k >= a.E.n) return;
@@ -398,7 +434,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
 
 // IC -> state (used once at create to build the reset template, n = 1)
 __global__ void f16_ic_kernel(SoA dst, const double* ic, ModelConsts C) {
-  __shared__ float sT[F16_BLOB_FLOATS];
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   stage_tables(sT);
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Lane L;
@@ -479,12 +515,23 @@ __device__ void trim_residual(const double* icb, const float* x, const float* T,
   ic[F16_IC_CMD_THR] = x[2];
   Lane L;
   apply_ic(L, ic, T, C);
+  // FGAccelerations::CalculateUVWdot: specific force + gravity - (pqr + 2 w_b) x uvw
+  // - Ti2b (w x (w x rI))
   Derived d;
   derive(L, 1.0, 0.0, d);
   float gb[3];
   mvec(d.Tec2b, d.gE, gb);
-  res[0] = L.ba[0] + gb[0];
-  res[1] = L.ba[2] + gb[2];
+  const float we = (float)OMEGA_E;
+  const float wb[3] = {d.Ti2b[2] * we, d.Ti2b[5] * we, d.Ti2b[8] * we};
+  const float t[3] = {d.pqr[0] + 2.0f * wb[0], d.pqr[1] + 2.0f * wb[1], d.pqr[2] + 2.0f * wb[2]};
+  float c1[3];
+  crossf(t, d.uvw, c1);
+  const double w2 = OMEGA_E * OMEGA_E;
+  const float wxwxr[3] = {(float)(-w2 * L.rI[0]), (float)(-w2 * L.rI[1]), 0.0f};
+  float cent[3];
+  mvec(d.Ti2b, wxwxr, cent);
+  res[0] = L.ba[0] + gb[0] - c1[0] - cent[0];
+  res[1] = L.ba[2] + gb[2] - c1[2] - cent[2];
   res[2] = L.wId[1];
 }
 __device__ void inv3f(const float* M, float* I, bool& ok) {
@@ -499,7 +546,7 @@ __device__ void inv3f(const float* M, float* I, bool& ok) {
 }
 __global__ __launch_bounds__(BLOCK) void f16_trim_kernel(int64_t n, const double* ic_in, double* ic_out,
                                                          double* resid, ModelConsts C) {
-  __shared__ float sT[F16_BLOB_FLOATS];
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   stage_tables(sT);
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (k >= n) return;
@@ -632,6 +679,8 @@ static void build_consts(const f16env_config& cfg, ModelConsts& C) {
   C.rho_sl = (float)(101325.0 / (R * 288.15) / 515.3788183931961);
   C.a_sl = (float)(sqrt(1.4 * R * 288.15) / 0.3048);
   C.p_sl = (float)(101325.0 / 47.88025898033584);
+  C.inv_rho_sl = (float)(1.0 / (101325.0 / (R * 288.15) / 515.3788183931961));
+  C.inv_p_sl = (float)(47.88025898033584 / 101325.0);
   C.kts_per_fps = (float)(1.0 / (1852.0 / (3600.0 * 0.3048)));
   C.dt = cfg.dt;
   C.cos_dE = cos(OMEGA_E * cfg.dt);
@@ -788,5 +837,16 @@ double f16env_algorithmic_bytes_per_env_step(int stack_k) {
 }
 
 const char* f16env_last_error(void) { return g_err.c_str(); }
+
+#ifdef F16_STAMPS
+// diagnostic build only: copy per-wave section cycle totals (waves x ST_N u64) to host
+int f16env_diag_stamps(unsigned long long* host, int max_waves) {
+  const int n = max_waves < (1 << 14) ? max_waves : (1 << 14);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * ST_N * n, 0,
+                             hipMemcpyDeviceToHost));
+  return ST_N;
+}
+#endif
 
 }  // extern "C"

@@ -20,7 +20,7 @@
  *
  * Deliberate, documented choices where the reference/JSBSim behaviour is undefined or
  * unavailable here (DESIGN.md "Model choices"):
- *   - RunIC = two evaluation passes without integration; FCS actuators settle on their
+ *   - RunIC = three evaluation passes without integration; FCS actuators settle on their
  *     commanded value (FGKinematic trim-mode semantics), PID derivative history primed,
  *     engine N2 at its target; then the integrator histories are filled
  *     (FGPropagate::InitializeDerivatives). Every reset is a full lane reset.
@@ -815,7 +815,11 @@ static void apply_ic(env_t* e, const double* ic, double dt) {
   for (int i = 0; i < F16L_N; i++) e->lx[i] = 0.0;
   for (int i = 0; i < 4; i++) e->cmd[i] = ic[F16_IC_CMD_AIL + i];
   for (int i = 0; i < 3; i++) e->wind[i] = ic[F16_IC_WIND_N_FPS + i];
-  /* two evaluation passes without integration, then InitializeDerivatives */
+  /* three evaluation passes without integration (the FCS reads the previous pass's
+   * auxiliary latch, whose n-pilot terms read the pass before's accelerations: three passes
+   * make FCS -> forces -> accelerations -> n-pilot -> FCS consistent), then
+   * InitializeDerivatives */
+  frame(e, dt, 1, NULL);
   frame(e, dt, 1, NULL);
   frame(e, dt, 1, NULL);
   for (int i = 0; i < 3; i++) {
@@ -1077,15 +1081,22 @@ static void trim_residual(const double* icb, const double* x, double dt, double*
   ic[F16_IC_CMD_ELE] = x[1];
   ic[F16_IC_CMD_THR] = x[2];
   apply_ic(&e, ic, dt);
-  /* body-axis acceleration (inertial accel rotated to body, minus the transport terms of a
-   * body moving with the rotating Earth, approximated by the body acceleration sum) */
+  /* FGAccelerations::CalculateUVWdot (body velocity wrt ECEF): specific force + gravity
+   * - (pqr + 2 w_b) x uvw - Ti2b (w x (w x rI)) */
   derived_t d;
   derive(&e, &d);
   double gE[3], gb[3];
   gravity_j2(&d, gE);
   mv(d.Tec2b, gE, gb);
-  res[0] = e.ba[0] + gb[0];
-  res[1] = e.ba[2] + gb[2];
+  double w[3] = {0, 0, OMEGA_E}, wb[3], c1[3], t[3], wxr[3], wxwxr[3], cent[3];
+  mv(d.Ti2b, w, wb);
+  for (int i = 0; i < 3; i++) t[i] = d.pqr[i] + 2.0 * wb[i];
+  cross(t, d.uvw, c1);
+  cross(w, e.rI, wxr);
+  cross(w, wxr, wxwxr);
+  mv(d.Ti2b, wxwxr, cent);
+  res[0] = e.ba[0] + gb[0] - c1[0] - cent[0];
+  res[1] = e.ba[2] + gb[2] - c1[2] - cent[2];
   res[2] = e.wId[1];
 }
 static void trim_one(const double* icb, double dt, double* ic_out, double* resid) {

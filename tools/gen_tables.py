@@ -332,6 +332,54 @@ def emit_kernel(model, path):
         put("eng_v_" + n, [v for r in t["data"] for v in r])
         eng_meta.append((n, len(t["rows"]), len(t["cols"])))
 
+    # ---- union grids (exact re-gridding: every original breakpoint is a union breakpoint,
+    # so the piecewise-linear, end-clamped functions are unchanged up to fp rounding) -------
+    def interp_clamped(rows, data, x):
+        if x <= rows[0]:
+            return data[0]
+        if x >= rows[-1]:
+            return data[-1]
+        i = 1
+        while i < len(rows) - 1 and rows[i] < x:
+            i += 1
+        f = (x - rows[i - 1]) / (rows[i] - rows[i - 1])
+        return data[i - 1] + f * (data[i] - data[i - 1])
+
+    mach_u = sorted({b for n in MACH_1D for b in fns[n]["table"]["rows"]})
+    put("machu_v", [interp_clamped(fns[n]["table"]["rows"], fns[n]["table"]["data"], x)
+                    for x in mach_u for n in MACH_1D])
+    eng_rows = model["engine"]["tables"]["AugThrust"]["rows"]
+    eng_cols = model["engine"]["tables"]["AugThrust"]["cols"]
+    eng_names = ("IdleThrust", "MilThrust", "AugThrust")
+    for n in eng_names:
+        t = model["engine"]["tables"][n]
+        assert t["cols"] == eng_cols
+        assert t["rows"] == eng_rows[:len(t["rows"])]
+    eng_u = []
+    for i in range(len(eng_rows)):
+        for j in range(len(eng_cols)):
+            for n in eng_names:
+                t = model["engine"]["tables"][n]
+                ii = min(i, len(t["rows"]) - 1)  # FGTable clamps the row factor at the last row
+                eng_u.append(t["data"][ii][j])
+    put("engu_v", eng_u)
+    # (lo, 1/span) pairs for LDS brackets (8-byte aligned for ds_read_b64)
+    if len(blob) % 2:
+        blob.append(0.0)
+
+    def pairs(bp):
+        out = []
+        for i in range(len(bp) - 1):
+            out += [bp[i], 1.0 / (bp[i + 1] - bp[i])]
+        return out
+    for key, bp in (("alpha", alpha_bp), ("de", de_bp), ("beta13", b13), ("beta7", b7),
+                    ("machu", mach_u), ("kclge", model["kCLge"]["rows"])):
+        put("pair_" + key, pairs(bp))
+    for n, t in model["fcs_tables"].items():
+        put("pair_fcs_" + n.split("/")[-1], pairs(t["rows"]))
+    if len(blob) % 2:
+        blob.append(0.0)
+
     L = ["/* GENERATED by tools/gen_tables.py from the reference's f16.xml / F100-PW-229.xml.",
          " * fp32 table blob staged into LDS by the step kernel. Do not edit by hand. */",
          "#pragma once", ""]
@@ -352,6 +400,13 @@ def emit_kernel(model, path):
     for n, nr in mach_meta:
         L.append("#define MACH_N_%s %d" % (n, nr))
     L.append("#define KCLGE_N %d" % len(model["kCLge"]["rows"]))
+    L.append("#define MACHU_N %d" % len(mach_u))
+    L.append("#define MACHU_NT %d" % len(MACH_1D))
+    for i, n in enumerate(MACH_1D):
+        L.append("#define MU_%s %d" % (n, i))
+    L.append("#define ENGU_NR %d" % len(eng_rows))
+    L.append("#define ENGU_NC %d" % len(eng_cols))
+    L.append("static constexpr float BP_machu[%d] = {%s};" % (len(mach_u), ", ".join(_lit(v, "%.9gf") for v in mach_u)))
     for n, t in model["fcs_tables"].items():
         L.append("#define FCS_N_%s %d" % (_cname(n.split("/")[-1]), len(t["rows"])))
     for n, nr, nc in eng_meta:
