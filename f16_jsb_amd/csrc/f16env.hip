@@ -242,6 +242,7 @@ struct StepArgs {
   int32_t* ep_len;
   int32_t* done_idx;
   int32_t* n_done;
+  int32_t lds_image;
   EnvArgs E;
   ModelConsts C;
 };
@@ -250,15 +251,41 @@ struct StepArgs {
 __device__ unsigned long long g_stamps[1 << 14][ST_N];  // per wave (diagnostic build)
 #endif
 
+// LDS-DMA of 16 B per lane: lane i's 16 bytes land at lds + 16*i (gfx950 global_load_lds_dwordx4)
+__device__ __forceinline__ void dma16(const float* g, float* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
+}
+
+// Dynamic LDS: image mode holds, per wave, the previous stack block of its 64 rows
+// (64*KC floats) + one spare frame; fallback mode holds the final/reset frames per lane.
+__device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t)64 * KC + 16; }
+
 __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
 #ifdef F16_STAMPS
   Stamps stamps = {};
   stamps.last = memtime();
 #endif
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
-  __shared__ float sF[BLOCK * FRAME_PITCH];   // final frame per lane
-  __shared__ float sR[BLOCK * FRAME_PITCH];   // reset frame per lane (done lanes)
   __shared__ int sDone[BLOCK];
+  extern __shared__ __align__(16) float dynl[];
+  const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
+  const int rows = (int)(a.E.n - row0 < 64 ? (a.E.n - row0 > 0 ? a.E.n - row0 : 0) : 64);
+  const bool image = a.lds_image != 0;
+  float* img = dynl + (size_t)wave * image_floats_per_wave(KC);
+  // 1) start the DMA of this wave's previous stack block into LDS (overlaps the physics)
+  if (image && rows > 0) {
+    const float* prev = a.obs_prev + row0 * KC;
+    const int total = rows * KC;  // floats
+    const int n16 = total >> 2;   // whole 16-byte pieces (wave blocks are 16-B aligned)
+    for (int b = 0; b < n16; b += 64) {
+      const int piece = b + lane;
+      if (piece < n16) dma16(prev + 4 * piece, img + 4 * b);
+    }
+    if (lane < (total & 3)) img[4 * n16 + lane] = prev[4 * n16 + lane];  // tail, never past the end
+  }
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = k < a.E.n;
   int done = 0;
@@ -269,6 +296,8 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
     av = reinterpret_cast<const float4*>(a.act)[k];
   }
   stage_tables(sT);
+  F16_STAMP(stamps, ST_LOAD);
+  float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
@@ -282,7 +311,6 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       se = sin(L.epa);
     }
     for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, sT, a.C, false F16_STAMP_PASS);  // :225-232
-    float f[F16_OBS_DIM];
     make_frame(L, ce, se, f);                                 // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261) in float32, then PositionReward (:493-507)
@@ -310,19 +338,14 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
     a.term[k] = (uint8_t)te;
     a.trunc[k] = (uint8_t)tr;
     done = te | tr;
-#pragma unroll
-    for (int j = 0; j < F16_OBS_DIM; ++j) sF[threadIdx.x * FRAME_PITCH + j] = f[j];
     if (done) {
       if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
       if (a.ep_len) a.ep_len[k] = L.step;
       if (!(a.E.flags & F16_FLAG_NO_AUTORESET)) {
-        float f0[F16_OBS_DIM];
         lane_reset(L, a.tmpl, nullptr, nullptr, a.E, k, sT, a.C, f0);
-#pragma unroll
-        for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f0[j];
       } else {
 #pragma unroll
-        for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f[j];
+        for (int j = 0; j < F16_OBS_DIM; ++j) f0[j] = f[j];
       }
     }
     F16_STAMP(stamps, ST_RESET);
@@ -333,7 +356,6 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
   // compaction of finished lanes (wave64 ballot)
   if (a.done_idx) {
     const unsigned long long m = __ballot(done);
-    const int lane = threadIdx.x & 63;
     int base = 0;
     if (m) {
       if (lane == 0) base = atomicAdd(a.n_done, __popcll(m));
@@ -341,26 +363,65 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
     }
   }
-  __syncthreads();
-  F16_STAMP(stamps, ST_SYNC);
-  // Ordered stack rebuild. A wave's 64 rows are one contiguous block of 64*K*15 floats in
-  // both obs_prev and obs, and out[j] = prev[j + 15] except in each row's last frame, so the
-  // wave walks the block with flat, coalesced indices j = lane + 64*it (row/col tracked
-  // incrementally, no division). Loads are issued in chunks of 16 before their stores so
-  // the latency overlaps; chunks only ever read ahead of what earlier chunks wrote, which
-  // keeps the in-place mode (obs_prev == obs) correct.
-  {
-    const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
-    const int64_t rows = a.E.n - row0 < 64 ? a.E.n - row0 : 64;
+  const bool autoreset = !(a.E.flags & F16_FLAG_NO_AUTORESET);
+  if (image) {
+    // 2) splice the new frame of row r into the image at row r+1's first frame, which the
+    //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (live) {
+      float* dst = img + (size_t)(lane + 1) * KC;
+#pragma unroll
+      for (int j = 0; j < F16_OBS_DIM; ++j) dst[j] = f[j];
+    }
+    __syncthreads();
+    // 3) finished rows: terminal obs = the spliced row; then the row becomes K x frame 0
+    if (live && done) {
+      float* src = img + (size_t)lane * KC + F16_OBS_DIM;
+      if (a.tobs) {
+        float* t = a.tobs + k * KC;
+        for (int c = 0; c < KC; ++c) t[c] = src[c];
+      }
+      if (autoreset)
+        for (int c = 0; c < KC; ++c) src[c] = f0[c % F16_OBS_DIM];
+    }
+    __syncthreads();
+    F16_STAMP(stamps, ST_SYNC);
+    // 4) one coalesced float4 copy of the block (obs blocks are 16-B aligned per wave)
+    if (rows > 0) {
+      float* out = a.obs + row0 * KC;
+      const int total = rows * KC, n4 = total >> 2;
+      float4* out4 = reinterpret_cast<float4*>(out);
+      for (int q = lane; q < n4; q += 64) {
+        const float* p = img + 4 * q + F16_OBS_DIM;
+        out4[q] = make_float4(p[0], p[1], p[2], p[3]);
+      }
+      for (int j = 4 * n4 + lane; j < total; j += 64) out[j] = img[j + F16_OBS_DIM];
+    }
+    F16_STAMP(stamps, ST_COPY);
+  } else {
+    // fallback (large K): chunked flat copy from obs_prev, frames staged in LDS
+    float* sF = dynl;
+    float* sR = dynl + BLOCK * FRAME_PITCH;
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < F16_OBS_DIM; ++j) sF[threadIdx.x * FRAME_PITCH + j] = f[j];
+      if (done)
+#pragma unroll
+        for (int j = 0; j < F16_OBS_DIM; ++j) sR[threadIdx.x * FRAME_PITCH + j] = f0[j];
+    }
+    __syncthreads();
+    F16_STAMP(stamps, ST_SYNC);
+    // A wave's 64 rows are one contiguous block of 64*K*15 floats in both obs_prev and obs,
+    // and out[j] = prev[j + 15] except in each row's last frame: the wave walks the block with
+    // flat, coalesced indices j = lane + 64*it; loads are issued in chunks of 16 before their
+    // stores, and chunks only read ahead of what earlier chunks wrote (in-place safe).
     if (rows > 0) {
       const float* prev = a.obs_prev + row0 * KC;
       float* out = a.obs + row0 * KC;
       float* tout = a.tobs ? a.tobs + row0 * KC : nullptr;
-      const bool autoreset = !(a.E.flags & F16_FLAG_NO_AUTORESET);
-      const int total = (int)rows * KC;
-      int row = lane / KC, col = lane - (lane / KC) * KC;  // one division, at start
+      const int total = rows * KC;
+      int row = lane / KC, col = lane - (lane / KC) * KC;
       constexpr int CH = 16;
       for (int base = 0; base < total; base += 64 * CH) {
         float v[CH];
@@ -393,10 +454,10 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
         }
       }
     }
+    F16_STAMP(stamps, ST_COPY);
   }
-  F16_STAMP(stamps, ST_COPY);
 #ifdef F16_STAMPS
-  if ((threadIdx.x & 63) == 0) {
+  if (lane == 0) {
     const int w = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
     if (w < (1 << 14))
       for (int q = 0; q < ST_N; ++q) g_stamps[w][q] = stamps.acc[q];
@@ -619,6 +680,8 @@ struct f16env {
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
+  int lds_image;   // step kernel stack-rebuild mode (LDS image when it fits)
+  size_t dyn_lds;  // dynamic LDS bytes per step-kernel block
 };
 
 static void soa_carve(void* base, int64_t n, SoA& s) {
@@ -741,6 +804,15 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     return set_err(-3, "hipMalloc(template) failed");
   }
   soa_carve(h->tmem, 1, h->tmpl);
+  {
+    const int KC = cfg->stack_k * F16_OBS_DIM;
+    const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
+    const size_t fallback = sizeof(float) * 2 * BLOCK * FRAME_PITCH;
+    const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + sizeof(int) * BLOCK + 64;
+    h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : 0;
+    h->dyn_lds = h->lds_image ? img : fallback;
+    hipFuncSetAttribute((const void*)f16_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
+  }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipLaunchKernelGGL(f16_ic_kernel, dim3(1), dim3(BLOCK), 0, 0, h->tmpl, (const double*)h->ic_dev, h->C);
   e = hipDeviceSynchronize();
@@ -793,8 +865,11 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
   a.done_idx = done_idx; a.n_done = n_done;
   a.E = env_args(h);
   a.C = h->C;
+  a.lds_image = h->lds_image;
+  if (((uintptr_t)obs & 15) != 0 || ((uintptr_t)obs_prev & 15) != 0)
+    return set_err(-1, "obs and obs_prev must be 16-byte aligned");
   if (n_done) HIPCHK(hipMemsetAsync(n_done, 0, sizeof(int32_t), (hipStream_t)stream));
-  hipLaunchKernelGGL(f16_step_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(f16_step_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), h->dyn_lds, (hipStream_t)stream, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
