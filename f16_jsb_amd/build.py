@@ -29,7 +29,8 @@ def build(verbose: bool = False, force: bool = False, extra=()) -> str:
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= t_out for d in DEPS):
             return OUT
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+    # -fno-slp-vectorize: packed-f32 pairing costs more v_mov than it saves at one wave/SIMD
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
            "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
            SRC, "-o", OUT + ".tmp", *extra]
     if verbose:

@@ -211,6 +211,8 @@ struct Seg {  // bracketing segment i-1..i and clamped factor
   float f;
 };
 __device__ __forceinline__ float rcpf(float x) { return __builtin_amdgcn_rcpf(x); }
+// v_sqrt_f32 (~1 ulp) for the physics; the env layer keeps IEEE sqrtf (bit-exact thresholds)
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 
 // FGTable::GetValue bracket: i = 1 + #{k in 1..N-2 : bp[k] < x} (literal compares), then the
@@ -236,6 +238,28 @@ __device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, i
   return {i, f};
 }
 __device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (b - a) + a; }
+
+// atan2 for finite arguments: octant reduction + odd minimax polynomial on [0, 1]
+// (|err| < 1e-7 rad, vs ~40 instructions + special-case handling for OCML atan2f)
+__device__ __forceinline__ float fatan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float a = (mx > 0.0f) ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+  const float s = a * a;
+  float p = 2.4566815505e-03f;
+  p = p * s - 1.4401176748e-02f;
+  p = p * s + 3.9780909971e-02f;
+  p = p * s - 7.2348286170e-02f;
+  p = p * s + 1.0498931099e-01f;
+  p = p * s - 1.4161224781e-01f;
+  p = p * s + 1.9985906079e-01f;
+  p = p * s - 3.3332596980e-01f;
+  p = p * s + 9.9999988637e-01f;
+  float r = a * p;
+  r = (ay > ax) ? 1.57079632679489662f - r : r;
+  r = (x < 0.0f) ? 3.14159265358979324f - r : r;
+  return copysignf(r, y);
+}
 
 // 1-D lookup over LDS values with literal breakpoints and LDS (lo, 1/span) pairs
 template <int N>
@@ -284,7 +308,7 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   o.T = T * 1.8f;
   o.P = P * (1.0f / 47.88025898033584f);
   o.rho = rho * (1.0f / 515.3788183931961f);
-  o.a = sqrtf(1.4f * R * T) * (1.0f / 0.3048f);
+  o.a = fsqrt(1.4f * R * T) * (1.0f / 0.3048f);
   return o;
 }
 
@@ -294,18 +318,18 @@ __device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts
   float pt;
   if (mach < 1.0f) {
     float x = 1.0f + 0.2f * mach * mach;
-    pt = p * (x * x * x * sqrtf(x));
+    pt = p * (x * x * x * fsqrt(x));
   } else {
     float m2 = mach * mach, d = 7.0f * m2 - 1.0f;
-    pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * sqrtf(d));
+    pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * fsqrt(d));
   }
   const float qc = pt - p;
   const float A = qc * C.inv_p_sl + 1.0f;
-  float M = sqrtf(5.0f * (__powf(A, 1.0f / 3.5f) - 1.0f));
+  float M = fsqrt(5.0f * (__powf(A, 1.0f / 3.5f) - 1.0f));
   if (M > 1.0f) {
     for (int i = 0; i < 10; ++i) {
       float t = 1.0f - rcpf(7.0f * M * M);
-      M = 0.8812848543473311f * sqrtf(A * (t * t * sqrtf(t)));
+      M = 0.8812848543473311f * fsqrt(A * (t * t * fsqrt(t)));
     }
   }
   return C.a_sl * M * C.kts_per_fps;
@@ -358,8 +382,15 @@ __device__ __forceinline__ void crossf(const float* a, const float* b, float* o)
   o[0] = x; o[1] = y; o[2] = z;
 }
 
-// geodetic altitude from ECEF (Fukushima 2006, one Halley step; FGLocation), fp64
-__device__ __forceinline__ double geodetic_altitude(double x, double y, double z, double rxy) {
+// Geodetic altitude from ECEF (Fukushima 2006, one Halley step; FGLocation), fp64, plus
+// the geodetic surface normal (for the per-step altitude reference below).
+struct AltRef {
+  double r0[3];  // ECEF position where h0 was evaluated exactly
+  double h0;
+  float n[3];    // geodetic up-normal there
+};
+__device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRef& A) {
+  const double rxy = sqrt(x * x + y * y);
   const double ec = WGS_B / WGS_A;
   const double s0 = fabs(z);
   const double zc = ec * s0, c0 = ec * rxy;
@@ -373,33 +404,49 @@ __device__ __forceinline__ double geodetic_altitude(double x, double y, double z
   const double cc = ec * (c1 * a03 - b0 * c0);
   const double s12 = s1 * s1, cc2 = cc * cc;
   const double norm = sqrt(s12 + cc2);
-  return (rxy * cc + s0 * s1 - WGS_A * sqrt(EC2 * s12 + cc2)) / norm;
-  (void)x; (void)y;
+  const double inv = 1.0 / norm;
+  A.h0 = (rxy * cc + s0 * s1 - WGS_A * sqrt(EC2 * s12 + cc2)) * inv;
+  const float cl = (float)(cc * inv), sl = (float)(s1 * inv) * (z < 0.0 ? -1.0f : 1.0f);
+  float clon = 1.0f, slon = 0.0f;
+  if (rxy != 0.0) {
+    const float ir = __builtin_amdgcn_rcpf((float)rxy);
+    clon = (float)x * ir;
+    slon = (float)y * ir;
+  }
+  A.n[0] = cl * clon; A.n[1] = cl * slon; A.n[2] = sl;
+  A.r0[0] = x; A.r0[1] = y; A.r0[2] = z;
 }
 
 // Everything FGPropagate / FGInertial derive from the integrated state.
 // ce, se: cos/sin of the Earth position angle (fp64).
-__device__ __forceinline__ void derive(const Lane& L, double ce, double se, Derived& d,
+// The geodetic altitude is evaluated exactly (fp64 Fukushima) once per env step (AltRef) and
+// advanced within the step along the geodetic normal: h = h0 + n . (rE - r0). Over one env
+// step |rE - r0| < 70 ft, so the neglected curvature term |dr|^2/2R < 2e-4 ft (far below the
+// 4e-4 ft fp32 resolution of the observed altitude).
+__device__ __forceinline__ void derive(const Lane& L, double ce, double se, const AltRef& A, Derived& d,
                                        float* lat_gc_out = nullptr, float* lon_out = nullptr) {
   const double xE = ce * L.rI[0] + se * L.rI[1];
   const double yE = -se * L.rI[0] + ce * L.rI[1];
   const double zE = L.rI[2];
-  const double rxy = sqrt(xE * xE + yE * yE);
-  d.h_ft = geodetic_altitude(xE, yE, zE, rxy);
+  {
+    const float dx = (float)(xE - A.r0[0]), dy = (float)(yE - A.r0[1]), dz = (float)(zE - A.r0[2]);
+    d.h_ft = A.h0 + (double)(A.n[0] * dx + A.n[1] * dy + A.n[2] * dz);
+  }
   // direction cosines only need fp32
-  const float xf = (float)xE, yf = (float)yE, zf = (float)zE, rxyf = (float)rxy;
-  const float rf = sqrtf(rxyf * rxyf + zf * zf);
+  const float xf = (float)xE, yf = (float)yE, zf = (float)zE;
+  const float rxyf = fsqrt(xf * xf + yf * yf);
+  const float rf = fsqrt(rxyf * rxyf + zf * zf);
   const float inv_r = rcpf(rf);
   const float slat = zf * inv_r, clat = rxyf * inv_r;
   float slon = 0.0f, clon = 1.0f;
-  if (rxy != 0.0) {
+  if (rxyf != 0.0f) {
     const float inv = rcpf(rxyf);
     slon = yf * inv;
     clon = xf * inv;
   }
   if (lat_gc_out) {
     *lat_gc_out = atan2f(zf, rxyf);
-    *lon_out = (rxy == 0.0) ? 0.0f : atan2f(yf, xf);
+    *lon_out = (rxyf == 0.0f) ? 0.0f : atan2f(yf, xf);
   }
   // Tec2l (geocentric, FGLocation)
   const float L0 = -clon * slat, L1 = -slon * slat, L2 = clat;
@@ -444,6 +491,12 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, Deri
   d.gE[2] = -gm * (1.0f + pre * zz) * slat;
 }
 
+__device__ __forceinline__ AltRef alt_ref(const Lane& L, double ce, double se) {
+  AltRef A;
+  alt_ref_init(ce * L.rI[0] + se * L.rI[1], -se * L.rI[0] + ce * L.rI[1], L.rI[2], A);
+  return A;
+}
+
 // Euler angles from Tl2b (FGMatrix33::GetEuler)
 __device__ __forceinline__ void euler(const float* T, float& phi, float& tht, float& psi) {
   if (T[2] <= -1.0f) {
@@ -464,35 +517,38 @@ __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fmi
 __device__ __forceinline__ bool eq_roundoff(float a, float b) {
   return fabsf(a - b) <= 2.0f * 1.1920929e-07f * fmaxf(fabsf(a), fabsf(b));
 }
-// FGKinematic with two detents (single segment): rate = (d1 - d0) / t
+// FGKinematic with two detents (single segment): rate = (d1 - d0) / t. Branch-free.
 __device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float rate, float dt,
                                       bool ic) {
   in = clipf(in, d0, d1);
-  if (ic) return in;
-  if (eq_roundoff(in, out)) return out;
+  if (ic) return in;  // compile-time after inlining
   const float tdt = fabsf((in - out) * (1.0f / rate));
-  if (dt < tdt) return (out < in) ? out + dt * rate : out - dt * rate;
-  return in;
+  const float step = (out < in) ? dt * rate : -dt * rate;
+  const float moved = (dt < tdt) ? out + step : in;
+  return eq_roundoff(in, out) ? out : moved;
 }
-// TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350)
+// TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350). The FGKinematic
+// while-loop needs at most three passes here (segment [-1,0] is instantaneous); unrolled,
+// branch-free.
 __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic) {
   in = clipf(in, -1.0f, 1.0f);
   if (ic) return in;
   float dt0 = dt;
-  for (int g = 0; g < 8 && dt0 > 0.0f && !eq_roundoff(in, out); ++g) {
-    // segment search (direction dependent), n = 3
-    const int ind = (in < out) ? ((0.0f < out) ? 2 : 1) : ((0.0f <= out) ? 2 : 1);
-    if (ind == 1) { out = in; break; }  // transition time 0 -> infinite rate
-    const float rate = 1.0f / 3.0f, lo = 0.0f, hi = 1.0f;
-    const float tin = clipf(in, lo, hi);
-    float tdt = fabsf((tin - out) * 3.0f);  // / rate, rate = 1/3
-    if (dt0 < tdt) {
-      tdt = dt0;
-      out = (out < in) ? out + tdt * rate : out - tdt * rate;
-    } else {
-      out = tin;
-    }
-    dt0 -= tdt;
+  bool active = true;
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    active = active && dt0 > 0.0f && !eq_roundoff(in, out);
+    const bool down = in < out;
+    const bool seg1 = down ? !(0.0f < out) : !(0.0f <= out);  // transition time 0 -> jump
+    const float tin = clipf(in, 0.0f, 1.0f);
+    const float tdt = fabsf((tin - out) * 3.0f);               // / rate, rate = 1/3
+    const bool partial = dt0 < tdt;
+    const float step = (out < in) ? dt0 * (1.0f / 3.0f) : -dt0 * (1.0f / 3.0f);
+    const float o1 = seg1 ? in : (partial ? out + step : tin);
+    const float d1 = (seg1 || partial) ? 0.0f : dt0 - tdt;
+    out = active ? o1 : out;
+    dt0 = active ? d1 : dt0;
+    active = active && !seg1;
   }
   return out;
 }
@@ -514,12 +570,24 @@ __device__ __forceinline__ float aero_scale(float in, float outmax) {
 struct FcsOut {
   float de, da, dr, dlef, flap_mix, dsb, throttle;
 };
+struct FcsTab {  // scheduled gains of the FCS, looked up from the previous frame's latch
+  float asc, ele, yaw;
+};
+__device__ __forceinline__ FcsTab fcs_tables(const Lane& L, const float* T) {
+  FcsTab t;
+  t.asc = tab1(BP_fcs_aileron_speed_compensated, T + OFF_pair_fcs_aileron_speed_compensated,
+               T + OFF_fcs_v_aileron_speed_compensated, L.lx[F16L_MACH]);
+  t.ele = tab1(BP_fcs_elevator_scheduler, T + OFF_pair_fcs_elevator_scheduler,
+               T + OFF_fcs_v_elevator_scheduler, L.lx[F16L_ALPHA]);
+  t.yaw = tab1(BP_fcs_yaw_rate_norm, T + OFF_pair_fcs_yaw_rate_norm, T + OFF_fcs_v_yaw_rate_norm,
+               L.lx[F16L_VG_FPS]);
+  return t;
+}
 
 // f16.xml:309-984 (document order). T = LDS table blob.
 __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33, float v_fps,
-                                        const float* T, float dt, bool ic, FcsOut& o) {
+                                        const float* T, const FcsTab& tb, float dt, bool ic, FcsOut& o) {
   const float alpha = L.lx[F16L_ALPHA], mach = L.lx[F16L_MACH], vc = L.lx[F16L_VC_KTS];
-  const float vg = L.lx[F16L_VG_FPS];
   // Flaps
   float tef_rad = 0.0f;
   if (vc < 250.0f) tef_rad = 0.349f;
@@ -532,16 +600,14 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
   o.da = aero_scale(roll_cmd, 0.375f);
   L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
-  const float asc = L.ail * tab1(BP_fcs_aileron_speed_compensated, T + OFF_pair_fcs_aileron_speed_compensated,
-                                 T + OFF_fcs_v_aileron_speed_compensated, mach);
+  const float asc = L.ail * tb.asc;
   const float lflap = clipf(-L.tef - asc, -1.0f, 1.0f);
   const float rflap = clipf(L.tef - asc, -1.0f, 1.0f);
   o.flap_mix = (lflap + rflap) * 1.4324f;
   // Pitch
   const float g_corr = L.lx[F16L_NPZ] - tl2b_33;  // cos(theta)cos(phi) == Tl2b(3,3)
   const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
-  const float ele_sched = ele_lim * tab1(BP_fcs_elevator_scheduler, T + OFF_pair_fcs_elevator_scheduler,
-                                         T + OFF_fcs_v_elevator_scheduler, alpha);
+  const float ele_sched = ele_lim * tb.ele;
   const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
   const float ele_trig = (vc < 5.0f) ? 0.0f : 1.0f;
   const float gpid = clipf(pidf(pitch_err, L.ppi, L.ppp, ele_trig, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
@@ -549,9 +615,7 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
   o.de = aero_scale(L.ele, 0.436f);
   // Yaw
-  const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tab1(BP_fcs_yaw_rate_norm, T + OFF_pair_fcs_yaw_rate_norm,
-                                                          T + OFF_fcs_v_yaw_rate_norm, vg) +
-                        L.lx[F16L_NPY] * 0.25f;
+  const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tb.yaw + L.lx[F16L_NPY] * 0.25f;
   const float rud_trig = (vc < 10.0f) ? 0.0f : 1.0f;
   const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, rud_trig, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
   const float yaw_sched = clipf(cmd[2] + ypid, -1.0f, 1.0f);
@@ -575,14 +639,9 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
 
 // FGTurbine tpRun, augmethod 2
 __device__ __forceinline__ float seekf(float v, float target, float accel, float decel, float dt) {
-  if (v > target) {
-    v -= dt * decel;
-    if (v < target) v = target;
-  } else if (v < target) {
-    v += dt * accel;
-    if (v > target) v = target;
-  }
-  return v;
+  const float dn = fmaxf(v - dt * decel, target);
+  const float up = fminf(v + dt * accel, target);
+  return (v > target) ? dn : ((v < target) ? up : v);
 }
 __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float mach, float h_rho,
                                             float sigma, const float* T, float dt, bool ic) {
@@ -721,19 +780,26 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 }
 
 // One FGFDMExec::Run(). ce/se: Earth angle cos/sin at the START of the frame (updated here).
-__device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se,
+// One FGFDMExec::Run(). ce/se: Earth angle cos/sin at the START of the frame (updated here).
+// Same arithmetic as the oracle's frame(), ordered for one wave's latency: the FCS gain
+// lookups (previous latch) are issued first, the wind-axis kinematics run while the fp64
+// altitude chain is in flight, and the calibrated airspeed (only read by the NEXT frame's
+// FCS) is computed last. No data-dependent branches except the rare large-rotation QExp
+// path and the supersonic vcas iteration.
+__device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se, const AltRef& A,
                                       const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
   const float dt = (float)C.dt;
+  const FcsTab tb = fcs_tables(L, T);
   if (!ic) {
     // -- FGPropagate: integrate with the previous frame's derivatives --
     const float hx = 0.5f * dt * L.wI[0], hy = 0.5f * dt * L.wI[1], hz = 0.5f * dt * L.wI[2];
     const float a2 = hx * hx + hy * hy + hz * hz;
-    float ca, sa;
-    if (a2 < 1e-2f) {  // |angle| < 0.1: series (error < 1e-11)
-      ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f)));
-      sa = 1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f)));
-    } else {
-      const float ang = sqrtf(a2);
+    // QExp: cos(a), sin(a)/a; series through a^8 (error < 3e-10 for |a| < 0.5, i.e. body
+    // rates below 120 rad/s), exact functions beyond
+    float ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f - a2 * (1.0f / 40320.0f))));
+    float sa = 1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f - a2 * (1.0f / 362880.0f))));
+    if (__builtin_expect(a2 >= 0.25f, 0)) {
+      const float ang = fsqrt(a2);
       ca = cosf(ang);
       sa = sinf(ang) / ang;
     }
@@ -766,50 +832,46 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   }
   F16_STAMP(stamps, ST_PROP);
   Derived d;
-  derive(L, ce, se, d);
+  derive(L, ce, se, A, d);
   F16_STAMP(stamps, ST_DERIVE);
-  // -- Atmosphere (standard day: density altitude == altitude) --
-  const float h = (float)d.h_ft;
-  const Atm atm = atmosphere(h);
-  const float sigma = atm.rho * C.inv_rho_sl;
-  F16_STAMP(stamps, ST_ATM);
-  // -- Systems --
-  FcsOut fc;
-  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, dt, ic, fc);
-  F16_STAMP(stamps, ST_FCS);
-  // -- Auxiliary --
+  // -- Auxiliary, wind-axis part (needs no atmosphere) --
   float wb[3];
   mvec(d.Tl2b, L.wind, wb);
   const float ua = d.uvw[0] - wb[0], va = d.uvw[1] - wb[1], wa = d.uvw[2] - wb[2];
   const float muw = ua * ua + wa * wa;
-  const float vt = sqrtf(muw + va * va);
-  const float alpha = muw > 0.0f ? atan2f(wa, ua) : 0.0f;
-  const float suw = sqrtf(muw);
-  const float beta = muw > 0.0f ? atan2f(va, suw) : 0.0f;
-  const float qbar = 0.5f * atm.rho * vt * vt;
-  const float mach = vt * rcpf(atm.a);
-  const float vc = vcas_kts(mach, atm.P, C);
-  const float vg = sqrtf(d.vned[0] * d.vned[0] + d.vned[1] * d.vned[1]);
-  float bi2vel = 0.0f, ci2vel = 0.0f;
-  if (vt != 0.0f) {
-    const float inv2v = 0.5f * rcpf(vt);
-    bi2vel = B_W * inv2v;
-    ci2vel = CBAR * inv2v;
-  }
+  const float vt = fsqrt(muw + va * va);
+  const bool moving = muw > 0.0f;
+  const float alpha = moving ? fatan2(wa, ua) : 0.0f;
+  const float suw = fsqrt(muw);
+  const float beta = moving ? fatan2(va, suw) : 0.0f;
+  const float iuw = rcpf(suw), ivt = rcpf(vt);
+  const float ca_ = moving ? ua * iuw : 1.0f, sa_ = moving ? wa * iuw : 0.0f;
+  const float cb_ = moving ? suw * ivt : 1.0f, sb_ = moving ? va * ivt : 0.0f;
+  const float inv2v = (vt != 0.0f) ? 0.5f * ivt : 0.0f;
+  const float bi2vel = B_W * inv2v, ci2vel = CBAR * inv2v;
+  const float vg = fsqrt(d.vned[0] * d.vned[0] + d.vned[1] * d.vned[1]);
+  // pilot-station load factors from the PREVIOUS frame's accelerations (FGAuxiliary runs
+  // before FGAccelerations)
   float t1[3], t2[3], t3[3];
   crossf(L.wId, C.eye, t1);
   crossf(L.wI, C.eye, t2);
   crossf(L.wI, t2, t3);
   const float npy = (L.ba[1] + t1[1] + t3[1]) * C.inv_gref;
   const float npz = (L.ba[2] + t1[2] + t3[2]) * C.inv_gref;
+  // -- Atmosphere (standard day: density altitude == altitude) --
+  const float h = (float)d.h_ft;
+  const Atm atm = atmosphere(h);
+  const float sigma = atm.rho * C.inv_rho_sl;
+  const float qbar = 0.5f * atm.rho * vt * vt;
+  const float mach = vt * rcpf(atm.a);
   // h_b-mac = (h - (Tb2l * rp)_down) / b
   const float vmac_d = d.Tl2b[2] * C.rp[0] + d.Tl2b[5] * C.rp[1] + d.Tl2b[8] * C.rp[2];
   const float hbmac = (h - vmac_d) * (1.0f / B_W);
-  L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;
-  L.lx[F16L_VC_KTS] = vc; L.lx[F16L_VG_FPS] = vg;
-  L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
-  L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
-  F16_STAMP(stamps, ST_AUX);
+  F16_STAMP(stamps, ST_ATM);
+  // -- Systems (reads the previous frame's latch) --
+  FcsOut fc;
+  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, tb, dt, ic, fc);
+  F16_STAMP(stamps, ST_FCS);
   // -- Propulsion --
   const float thrust = engine_run(L, fc.throttle, mach, h, sigma, T, dt, ic);
   F16_STAMP(stamps, ST_ENGINE);
@@ -823,13 +885,6 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   float A6[6];
   aero(ai, T, A6);
   // wind (D, Y, L) -> body, vFw = (-D, Y, -L)
-  float ca_ = 1.0f, sa_ = 0.0f, cb_ = 1.0f, sb_ = 0.0f;
-  if (muw > 0.0f) {
-    const float iuw = rcpf(suw);
-    ca_ = ua * iuw; sa_ = wa * iuw;
-    const float ivt = rcpf(vt);
-    cb_ = suw * ivt; sb_ = va * ivt;
-  }
   const float fw0 = -A6[0], fw1 = A6[1], fw2 = -A6[2];
   float F[3], M[3];
   F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
@@ -858,6 +913,11 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
 #pragma unroll
   for (int j = 0; j < 3; ++j) rhs[j] = M[j] - wxJw[j];
   mvec(C.Jinv, rhs, L.wId);
+  // -- Auxiliary latch for the next frame's FCS --
+  L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;
+  L.lx[F16L_VC_KTS] = vcas_kts(mach, atm.P, C); L.lx[F16L_VG_FPS] = vg;
+  L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
+  L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
   F16_STAMP(stamps, ST_ACCEL);
 }
 

@@ -143,9 +143,10 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
 #ifdef F16_STAMPS
   Stamps stamps = {};
 #endif
-  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);  // three passes, as oracle apply_ic()
-  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);
-  frame(L, cmd, ce, se, T, C, true F16_STAMP_PASS);
+  const AltRef A = alt_ref(L, ce, se);
+  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);  // three passes, as oracle apply_ic()
+  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
+  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
   for (int j = 0; j < 3; ++j) { L.dv1[j] = 0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }
 }
 
@@ -163,10 +164,10 @@ __device__ __forceinline__ float norm_angle(float a) {
   return (float)x;
 }
 // _get_current_single_observation (jsbsim_gym.py:172-197)
-__device__ void make_frame(const Lane& L, double ce, double se, float* f) {
+__device__ void make_frame(const Lane& L, double ce, double se, const AltRef& A, float* f) {
   Derived d;
   float lat, lon;
-  derive(L, ce, se, d, &lat, &lon);
+  derive(L, ce, se, A, d, &lat, &lon);
   float phi, tht, psi;
   euler(d.Tl2b, phi, tht, psi);
   f[0] = (float)((double)lat * 6.3781e6);
@@ -214,7 +215,7 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
-  make_frame(L, 1.0, 0.0, f0);
+  make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
 }
 
@@ -310,8 +311,9 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       ce = cos(L.epa);
       se = sin(L.epa);
     }
-    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, sT, a.C, false F16_STAMP_PASS);  // :225-232
-    make_frame(L, ce, se, f);                                 // :234
+    const AltRef A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
+    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    make_frame(L, ce, se, A, f);                              // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261) in float32, then PositionReward (:493-507)
     float r32;
@@ -579,7 +581,7 @@ __device__ void trim_residual(const double* icb, const float* x, const float* T,
   // FGAccelerations::CalculateUVWdot: specific force + gravity - (pqr + 2 w_b) x uvw
   // - Ti2b (w x (w x rI))
   Derived d;
-  derive(L, 1.0, 0.0, d);
+  derive(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), d);
   float gb[3];
   mvec(d.Tec2b, d.gE, gb);
   const float we = (float)OMEGA_E;

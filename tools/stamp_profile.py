@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--stack", type=int, default=4)
     args = ap.parse_args()
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
-                    "-DF16_STAMPS", "-shared", "-fPIC", "-Wno-unused-value",
+                    "-DF16_STAMPS", "-shared", "-fPIC", "-Wno-unused-value", "-fno-slp-vectorize",
                     os.path.join(ROOT, "f16_jsb_amd", "csrc", "f16env.hip"), "-o", DIAG], check=True)
     os.environ["F16ENV_LIB"] = DIAG
     sys.path.insert(0, ROOT)
