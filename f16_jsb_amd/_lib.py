@@ -46,13 +46,15 @@ def lib():
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
     L.f16env_sample_actions.argtypes = [vp, vp, u64, u64, vp]
+    L.f16env_gae.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, ctypes.c_double,
+                             ctypes.c_double, vp, vp]
     L.f16env_step_kernel_name.restype = ctypes.c_char_p
     L.f16env_algorithmic_bytes_per_env_step.argtypes = [i32]
     L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
     L.f16env_last_error.restype = ctypes.c_char_p
     for name in ("f16env_config_default", "f16env_create", "f16env_destroy", "f16env_reset",
                  "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
-                 "f16env_sample_actions"):
+                 "f16env_sample_actions", "f16env_gae"):
         getattr(L, name).restype = i32
     _lib = L
     return L
@@ -68,6 +70,6 @@ def check(status: int, what: str):
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_get_state",
-    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_step_kernel_name",
+    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_step_kernel_name",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
 )

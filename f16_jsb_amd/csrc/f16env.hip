@@ -670,6 +670,33 @@ __global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t s
   reinterpret_cast<float4*>(act)[k] = v;
 }
 
+// GAE(lambda) over a [n_steps][n_envs] rollout, one lane per env, backward in time.
+// Restates stable_baselines3/common/buffers.py:403-438 (RolloutBuffer.
+// compute_returns_and_advantage) with numpy's float32 per-operation rounding: every product
+// and sum is rounded separately (no FMA), gamma and gamma*lambda are rounded to float32
+// exactly as numpy casts a Python float against a float32 array.
+__global__ void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __restrict__ rewards,
+                               const float* __restrict__ values, const float* __restrict__ ep_starts,
+                               const float* __restrict__ last_values, const uint8_t* __restrict__ dones,
+                               float g, float gl, float* __restrict__ adv, float* __restrict__ ret) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_envs) return;
+  float lgl = 0.0f;
+  float nv = last_values[e];
+  float nnt = __fsub_rn(1.0f, dones[e] ? 1.0f : 0.0f);
+  for (int64_t s = n_steps - 1; s >= 0; --s) {
+    const int64_t i = s * n_envs + e;
+    const float v = values[i];
+    const float t2 = __fmul_rn(__fmul_rn(g, nv), nnt);
+    const float delta = __fsub_rn(__fadd_rn(rewards[i], t2), v);
+    lgl = __fadd_rn(delta, __fmul_rn(__fmul_rn(gl, nnt), lgl));
+    adv[i] = lgl;
+    ret[i] = __fadd_rn(lgl, v);
+    nv = v;
+    nnt = __fsub_rn(1.0f, ep_starts[i]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -903,6 +930,19 @@ int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step
   if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
   hipLaunchKernelGGL(f16_sample_actions_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream,
                      (int64_t)h->soa.n, (int64_t)h->cfg.env_id_base, seed, step, act);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
+               const float* episode_starts, const float* last_values, const uint8_t* dones, double gamma,
+               double gae_lambda, float* advantages, float* returns) {
+  if (n_steps <= 0 || n_envs <= 0) return set_err(-1, "n_steps and n_envs must be > 0");
+  if (!rewards || !values || !episode_starts || !last_values || !dones || !advantages || !returns)
+    return set_err(-1, "null argument");
+  const float g = (float)gamma, gl = (float)(gamma * gae_lambda);
+  hipLaunchKernelGGL(f16_gae_kernel, dim3((unsigned)((n_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_steps, n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
   HIPCHK(hipGetLastError());
   return 0;
 }

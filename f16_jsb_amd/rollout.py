@@ -1,0 +1,157 @@
+"""Device-resident PPO rollout storage, GAE and the rank-0 gather (BASELINE cfg 4).
+
+The caller side of the hot path: SB3's `collect_rollouts`
+(on_policy_algorithm.py:162-268) fills a numpy `RolloutBuffer` (buffers.py:343-522) one env at
+a time. Here the buffer lives in HBM as [n_steps][n_envs] tensors, GAE runs as the HIP kernel
+`f16env_gae` (bit-exact with buffers.py:403-438's float32 numpy recurrence), and after a
+rollout every rank's shard lands on rank 0 with RCCL gathers over xGMI
+(`torch.distributed` backend "nccl" is RCCL on ROCm).
+
+Frame dedup: a stacked observation is K overlapping frames, so the buffer keeps
+only the newest frame per step plus the stack before step 0, and rebuilds any step's stack
+from those and `episode_starts` (a reset observation is K copies of its first frame). That
+cuts the gathered observation bytes by K.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from .abi import F16_OBS_DIM
+
+FIELDS = ("frames", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns")
+
+
+class DeviceRolloutBuffer:
+    def __init__(self, n_steps: int, n_envs: int, stack_k: int, device, gamma: float = 0.99,
+                 gae_lambda: float = 0.95, act_dim: int = 4):
+        self.n_steps, self.n_envs, self.k = int(n_steps), int(n_envs), int(stack_k)
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        self.device = torch.device(device)
+        f32 = torch.float32
+        z = lambda *s: torch.zeros(*s, dtype=f32, device=self.device)  # noqa: E731
+        self.frames = z(self.n_steps, self.n_envs, F16_OBS_DIM)       # newest frame of obs[t]
+        self.obs0 = z(self.n_envs, self.k, F16_OBS_DIM)                # full stack of obs[0]
+        self.actions = z(self.n_steps, self.n_envs, act_dim)
+        self.rewards = z(self.n_steps, self.n_envs)
+        self.episode_starts = z(self.n_steps, self.n_envs)
+        self.values = z(self.n_steps, self.n_envs)
+        self.log_probs = z(self.n_steps, self.n_envs)
+        self.advantages = z(self.n_steps, self.n_envs)
+        self.returns = z(self.n_steps, self.n_envs)
+        self.pos = 0
+
+    def reset(self):
+        self.pos = 0
+
+    @property
+    def full(self) -> bool:
+        return self.pos == self.n_steps
+
+    def add(self, obs, action, reward, episode_start, value, log_prob):
+        """RolloutBuffer.add (buffers.py:440-479) with device tensors; obs is (N, K, 15)."""
+        if self.pos >= self.n_steps:
+            raise RuntimeError("rollout buffer is full")
+        t = self.pos
+        if t == 0:
+            self.obs0.copy_(obs)
+        self.frames[t].copy_(obs[:, -1])
+        self.actions[t].copy_(action.reshape(self.n_envs, -1))
+        self.rewards[t].copy_(reward.reshape(-1))
+        self.episode_starts[t].copy_(episode_start.reshape(-1).to(torch.float32))
+        self.values[t].copy_(value.reshape(-1))
+        self.log_probs[t].copy_(log_prob.reshape(-1))
+        self.pos += 1
+
+    def compute_returns_and_advantage(self, last_values, dones, stream=None):
+        """buffers.py:403-438 on the GPU (HIP kernel f16env_gae)."""
+        from ._lib import check, lib
+
+        if self.device.type != "cuda":
+            raise RuntimeError("GAE runs on the GPU (f16env_gae); buffer is on %s" % self.device)
+        lv = last_values.reshape(-1).to(torch.float32).contiguous()
+        dn = dones.reshape(-1).to(torch.uint8).contiguous()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().f16env_gae(ctypes.c_void_p(s), self.n_steps, self.n_envs, self.rewards.data_ptr(),
+                               self.values.data_ptr(), self.episode_starts.data_ptr(), lv.data_ptr(),
+                               dn.data_ptr(), self.gamma, self.gae_lambda, self.advantages.data_ptr(),
+                               self.returns.data_ptr()), "f16env_gae")
+
+    # ----------------------------------------------------------------------------------------
+    def observations(self, steps=None):
+        return rebuild_observations(self.frames, self.obs0, self.episode_starts, self.k, steps)
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {f: getattr(self, f) for f in FIELDS} | {"obs0": self.obs0}
+
+
+def bootstrap_timeouts(rewards, terminated, truncated, terminal_values, gamma: float):
+    """on_policy_algorithm.py:236-245 vectorised: for lanes that ended by truncation only,
+    rewards += gamma * V(terminal_observation) (float32 per-op rounding as SB3)."""
+    mask = truncated.bool() & ~terminated.bool()
+    g = torch.tensor(gamma, dtype=torch.float32, device=rewards.device)
+    add = g * terminal_values.reshape(-1).to(torch.float32)
+    return torch.where(mask, rewards + add, rewards)
+
+
+def rebuild_observations(frames, obs0, episode_starts, k: int, steps=None):
+    """Stacked observations (T, N, K, 15) from newest frames, the initial stack and
+    episode starts: obs[t][j] = frame[max(t - (K-1) + j, s_t)] where s_t is the last episode
+    start <= t; indices before step 0 come from the initial stack (oldest first)."""
+    T, N, D = frames.shape
+    dev = frames.device
+    tt = torch.arange(T, device=dev)
+    if steps is None:
+        steps = tt
+    steps = torch.as_tensor(steps, device=dev)
+    # last episode start at or before t, per env (-inf if none)
+    marks = torch.where(episode_starts.bool(), tt[:, None].expand(T, N), torch.full((T, N), -(1 << 30), device=dev))
+    last_start = torch.cummax(marks, dim=0).values                      # (T, N)
+    j = torch.arange(k, device=dev)
+    src = steps[:, None] - (k - 1) + j[None, :]                          # (S, K)
+    ls = last_start[steps]                                               # (S, N)
+    idx = torch.maximum(src[:, None, :], ls[:, :, None])                # (S, N, K)
+    from_frames = idx >= 0
+    fi = idx.clamp(min=0)
+    e = torch.arange(N, device=dev)[None, :, None].expand_as(fi)
+    out_f = frames[fi, e]                                                # (S, N, K, D)
+    oi = (idx + (k - 1)).clamp(0, k - 1)                                 # position in obs0
+    out_0 = obs0[e, oi]                                                  # (S, N, K, D)
+    return torch.where(from_frames[..., None], out_f, out_0)
+
+
+def gather_to_rank0(buf: DeviceRolloutBuffer, group=None, chunk_steps: Optional[int] = None,
+                    fields=FIELDS) -> Optional[Dict[str, torch.Tensor]]:
+    """Gather every rank's rollout shard to rank 0 (RCCL over xGMI on MI355X, gloo in CPU
+    tests). Returns on rank 0 a dict of (n_steps, world*n_envs, ...) tensors (env axis
+    rank-major, matching env_id_base = rank * n_envs) plus 'obs0'; None on other ranks.
+    Gathers are chunked over steps (chunk_steps) to bound the staging memory."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    T = buf.n_steps
+    chunk = T if not chunk_steps else max(1, int(chunk_steps))
+    out = {}
+    for f in tuple(fields) + ("obs0",):
+        x = getattr(buf, f)
+        if f == "obs0":
+            parts = [torch.empty_like(x) for _ in range(world)] if rank == 0 else None
+            dist.gather(x.contiguous(), parts, dst=0, group=group)
+            if rank == 0:
+                out[f] = torch.cat(parts, dim=0)
+            continue
+        res = torch.empty((T, world * buf.n_envs) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device) if rank == 0 else None
+        for t0 in range(0, T, chunk):
+            t1 = min(T, t0 + chunk)
+            piece = x[t0:t1].contiguous()
+            parts = [torch.empty_like(piece) for _ in range(world)] if rank == 0 else None
+            dist.gather(piece, parts, dst=0, group=group)
+            if rank == 0:
+                for r in range(world):
+                    res[t0:t1, r * buf.n_envs:(r + 1) * buf.n_envs] = parts[r]
+        if rank == 0:
+            out[f] = res
+    return out if rank == 0 else None

@@ -177,6 +177,14 @@ int f16env_trim(f16env_t h, void* stream, const double* ic_in, double* ic_out,
  * (seed; global env id, step). act: N x 4 float. */
 int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step, float* act);
 
+/* GAE(lambda) advantages and returns over a device rollout laid out [n_steps][n_envs]
+ * (float32; episode_starts as 0/1 float, dones uint8 for the step after the last), restating
+ * stable_baselines3/common/buffers.py:403-438 RolloutBuffer.compute_returns_and_advantage
+ * bit for bit (numpy float32 per-operation rounding). No handle needed. */
+int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
+               const float* episode_starts, const float* last_values, const uint8_t* dones, double gamma,
+               double gae_lambda, float* advantages, float* returns);
+
 /* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
  * HBM bytes one env-step moves. */
 const char* f16env_step_kernel_name(void);
