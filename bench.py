@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--action-pool", type=int, default=0,
                     help="distinct pre-generated action batches (0 = one per timed step)")
+    ap.add_argument("--rollout-envs", type=int, default=32768, help="cfg4 rollout envs per GPU (0 = skip)")
+    ap.add_argument("--rollout-steps", type=int, default=2048, help="cfg4 PPO n_steps")
+    ap.add_argument("--gather-chunk", type=int, default=256, help="steps per RCCL gather chunk")
     return ap.parse_args()
 
 
@@ -76,6 +79,71 @@ def cpu_baseline(envs, stack, seconds):
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
                       "%d envs x %d random-action steps (stack=%d, auto-reset), %d OpenMP threads, %.1f s"
                       % (n, steps, stack, threads, el)}
+
+
+def rollout_bench(args, dev, rank, world):
+    """BASELINE cfg4 beside the headline: a PPO-shaped rollout (n_steps x envs per GPU) into
+    the device rollout buffer, HIP GAE, then the RCCL gather of every shard to rank 0.
+    Rollout, GAE and gather are timed separately (max over ranks); not part of `value`."""
+    import torch
+    import torch.distributed as dist
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout, gather_to_rank0
+
+    n, T = args.rollout_envs, args.rollout_steps
+    envs = F16Envs(n, stack_k=args.stack, device=dev, seed=args.seed + 7, env_id_base=rank * n)
+    envs.reset()
+    buf = DeviceRolloutBuffer(T, n, args.stack, dev)
+    collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), args.seed + 3000)  # warm
+    sync = torch.cuda.synchronize
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        sync()
+
+    barrier()
+    t0 = time.perf_counter()
+    last_v, last_d = collect_rollout(envs, buf, args.seed + 4000)
+    sync()
+    t1 = time.perf_counter()
+    buf.compute_returns_and_advantage(last_v, last_d)
+    sync()
+    t2 = time.perf_counter()
+    gathered = 0
+    t_gather = 0.0
+    if world > 1:
+        small = DeviceRolloutBuffer(2, 64, args.stack, dev)
+        gather_to_rank0(small)  # communicator warm-up
+        barrier()
+        t3 = time.perf_counter()
+        out = gather_to_rank0(buf, chunk_steps=args.gather_chunk)
+        barrier()
+        t_gather = time.perf_counter() - t3
+        if rank == 0:
+            gathered = sum(v.numel() * v.element_size() for v in out.values())
+        del out
+    tt = torch.tensor([t1 - t0, t2 - t1, t_gather], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    shard_bytes = sum(v.numel() * v.element_size() for v in buf.state_dict().values())
+    envs.close()
+    del buf
+    torch.cuda.empty_cache()
+    r = {
+        "workload": "BASELINE cfg4: %d envs/GPU x %d GPUs, PPO n_steps=%d, stack=%d, random policy (device "
+                    "Philox; values/log-probs zero: policy network out of scope)" % (n, world, T, args.stack),
+        "rollout_s": round(float(tt[0]), 4),
+        "rollout_env_steps_per_s": round(n * world * T / float(tt[0]), 1),
+        "gae_ms": round(float(tt[1]) * 1e3, 3),
+        "shard_bytes_per_rank": shard_bytes,
+        "gather_s": round(float(tt[2]), 4) if world > 1 else None,
+        "gather_bytes_at_rank0": gathered if world > 1 else None,
+        "gather_GBps_at_rank0": round(gathered / float(tt[2]) / 1e9, 2) if world > 1 and tt[2] > 0 else None,
+        "gather": "RCCL dist.gather, %d-step chunks, frame-deduplicated obs (newest frame + initial stack)"
+                  % args.gather_chunk if world > 1 else "n/a (1 GPU)",
+    }
+    return r
 
 
 def load_traffic(envs, stack):
@@ -161,6 +229,12 @@ def main():
         tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, gpu_ms_per_step = float(tt[0]), float(tt[1]), float(tt[2])
+    venv.close()
+    del acts, warm
+    torch.cuda.empty_cache()
+    rollout = None
+    if args.rollout_envs > 0 and args.rollout_steps > 0:
+        rollout = rollout_bench(args, dev, rank, world)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -213,6 +287,8 @@ def main():
         },
         "done_fraction_last_step": round(done_frac, 5),
     }
+    if rollout is not None:
+        out["rollout"] = rollout
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds)
     print(json.dumps(out), flush=True)

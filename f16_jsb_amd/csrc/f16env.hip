@@ -679,21 +679,23 @@ __global__ void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __r
                                const float* __restrict__ values, const float* __restrict__ ep_starts,
                                const float* __restrict__ last_values, const uint8_t* __restrict__ dones,
                                float g, float gl, float* __restrict__ adv, float* __restrict__ ret) {
+  // float32 per-op rounding as numpy (no FMA contraction; __f*_rn still contract under -O3)
+#pragma clang fp contract(off)
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_envs) return;
   float lgl = 0.0f;
   float nv = last_values[e];
-  float nnt = __fsub_rn(1.0f, dones[e] ? 1.0f : 0.0f);
+  float nnt = 1.0f - (dones[e] ? 1.0f : 0.0f);
   for (int64_t s = n_steps - 1; s >= 0; --s) {
     const int64_t i = s * n_envs + e;
     const float v = values[i];
-    const float t2 = __fmul_rn(__fmul_rn(g, nv), nnt);
-    const float delta = __fsub_rn(__fadd_rn(rewards[i], t2), v);
-    lgl = __fadd_rn(delta, __fmul_rn(__fmul_rn(gl, nnt), lgl));
+    const float t2 = (g * nv) * nnt;
+    const float delta = (rewards[i] + t2) - v;
+    lgl = delta + (gl * nnt) * lgl;
     adv[i] = lgl;
-    ret[i] = __fadd_rn(lgl, v);
+    ret[i] = lgl + v;
     nv = v;
-    nnt = __fsub_rn(1.0f, ep_starts[i]);
+    nnt = 1.0f - ep_starts[i];
   }
 }
 

@@ -87,6 +87,35 @@ class DeviceRolloutBuffer:
         return {f: getattr(self, f) for f in FIELDS} | {"obs0": self.obs0}
 
 
+def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None):
+    """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors with random
+    policy actions from the device Philox stream (the policy network is out of scope; values
+    and log-probs are zeros unless ``values_fn(obs) -> (values, log_probs)`` is given).
+    Starts from envs' current observation; returns (last_values, last_dones) for GAE."""
+    dev = buf.device
+    n = buf.n_envs
+    zeros = torch.zeros(n, dtype=torch.float32, device=dev)
+    obs = envs.obs
+    starts = getattr(envs, "_last_episode_starts", None)
+    if starts is None:
+        starts = torch.ones(n, dtype=torch.float32, device=dev)
+    buf.reset()
+    for t in range(buf.n_steps):
+        act = envs.sample_actions(seed, step0 + t)
+        v, lp = values_fn(obs) if values_fn is not None else (zeros, zeros)
+        out = envs.step(act)
+        rew = out.rew
+        if values_fn is not None:
+            tv, _ = values_fn(out.terminal_obs)
+            rew = bootstrap_timeouts(rew, out.terminated, out.truncated, tv, buf.gamma)
+        buf.add(obs, act, rew, starts, v, lp)
+        obs = out.obs
+        starts = (out.terminated | out.truncated).to(torch.float32)
+    envs._last_episode_starts = starts
+    last_v = values_fn(obs)[0] if values_fn is not None else zeros
+    return last_v, starts
+
+
 def bootstrap_timeouts(rewards, terminated, truncated, terminal_values, gamma: float):
     """on_policy_algorithm.py:236-245 vectorised: for lanes that ended by truncation only,
     rewards += gamma * V(terminal_observation) (float32 per-op rounding as SB3)."""
