@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3",
+                    help="cfg3: the headline (reference task); cfg5: random ICs + wind gusts")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (cfg3 65536, cfg5 131072)")
     ap.add_argument("--stack", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
@@ -51,7 +53,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(envs, stack, seconds):
+def cpu_baseline(envs, stack, seconds, cfg5=False):
     """Time the fp64 CPU oracle on the same workload (random actions, auto-reset)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     try:
@@ -63,7 +65,7 @@ def cpu_baseline(envs, stack, seconds):
     import numpy as np
     threads = int(lib().f16ref_threads())
     n = min(envs, 65536)
-    e = OracleEnvs(n, stack_k=stack, seed=1)
+    e = OracleEnvs(n, stack_k=stack, seed=1, cfg5=cfg5)
     e.reset()
     steps = 0
     t0 = time.perf_counter()
@@ -77,8 +79,8 @@ def cpu_baseline(envs, stack, seconds):
     e.close()
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
-                      "%d envs x %d random-action steps (stack=%d, auto-reset), %d OpenMP threads, %.1f s"
-                      % (n, steps, stack, threads, el)}
+                      "%d envs x %d random-action steps (stack=%d, auto-reset%s), %d OpenMP threads, %.1f s"
+                      % (n, steps, stack, ", cfg5 random IC + gusts" if cfg5 else "", threads, el)}
 
 
 def rollout_bench(args, dev, rank, world):
@@ -181,9 +183,12 @@ def main():
     if world > 1:
         dist.barrier()
 
+    cfg5 = args.workload == "cfg5"
+    if args.envs is None:
+        args.envs = 131072 if cfg5 else 65536
     n = args.envs
     venv = F16VecEnv(num_envs=n, stack_k=args.stack, device=dev, seed=args.seed, return_numpy=False,
-                     env_id_base=rank * n)
+                     env_id_base=rank * n, cfg5=cfg5)
     envs = venv.envs
     venv.reset()
     pool = args.action_pool if args.action_pool > 0 else args.steps
@@ -233,7 +238,7 @@ def main():
     del acts, warm
     torch.cuda.empty_cache()
     rollout = None
-    if args.rollout_envs > 0 and args.rollout_steps > 0:
+    if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
         rollout = rollout_bench(args, dev, rank, world)
 
     if rank != 0:
@@ -241,14 +246,14 @@ def main():
         return
     total_env_steps = n * world * args.steps
     value = total_env_steps / elapsed
-    bytes_per_env_step = envs.algorithmic_bytes_per_env_step()
+    bytes_per_env_step = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
     bytes_per_launch = bytes_per_env_step * n
     # launch duration used for the roofline: GPU time of the timed region / launches (the
     # region is back-to-back f16_step_kernel launches; includes ~1-2 us dispatch gaps, so it
     # bounds the rocprof kernel duration from above). The per-launch event median (which also
     # counts event overhead) is reported beside it.
     achieved = bytes_per_launch / (gpu_ms_per_step * 1e-3) / 1e9
-    traffic = load_traffic(n, args.stack)
+    traffic = None if cfg5 else load_traffic(n, args.stack)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -263,8 +268,11 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": "BASELINE cfg3: %d F-16 envs per MI355X, waypoint-goal task, stack=%d, random actions "
-                        "(device Philox, pre-generated in HBM), auto-reset on done" % (n, args.stack),
+            "workload": ("BASELINE cfg5: %d F-16 envs per MI355X, randomised ICs + Gauss-Markov wind gusts, "
+                         "stack=%d, random actions (device Philox, pre-generated in HBM), auto-reset to a new "
+                         "random IC on done" if cfg5 else
+                         "BASELINE cfg3: %d F-16 envs per MI355X, waypoint-goal task, stack=%d, random actions "
+                         "(device Philox, pre-generated in HBM), auto-reset on done") % (n, args.stack),
             "envs_per_gpu": n,
             "global_envs": n * world,
             "stack_k": args.stack,
@@ -278,7 +286,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
-            "kernel": "f16_step_kernel",
+            "kernel": "f16_step_cfg5_kernel<3> + f16_reset_done_kernel" if cfg5 else "f16_step_kernel",
             "kernel_ms": round(gpu_ms_per_step, 5),
             "kernel_timing": "HIP events around the timed region on the launch stream / launches",
             "kernel_ms_event_pair_median": round(kern_ms, 5),
@@ -290,7 +298,7 @@ def main():
     if rollout is not None:
         out["rollout"] = rollout
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

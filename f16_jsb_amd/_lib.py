@@ -35,6 +35,7 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, u64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
     L.f16env_config_default.argtypes = [ctypes.POINTER(EnvConfig)]
+    L.f16env_config_cfg5.argtypes = [ctypes.POINTER(EnvConfig)]
     L.f16env_create.argtypes = [ctypes.POINTER(EnvConfig), i32, ctypes.POINTER(vp)]
     L.f16env_destroy.argtypes = [vp]
     L.f16env_state_bytes.argtypes = [vp]
@@ -52,7 +53,7 @@ def lib():
     L.f16env_algorithmic_bytes_per_env_step.argtypes = [i32]
     L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
     L.f16env_last_error.restype = ctypes.c_char_p
-    for name in ("f16env_config_default", "f16env_create", "f16env_destroy", "f16env_reset",
+    for name in ("f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_reset",
                  "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
                  "f16env_sample_actions", "f16env_gae"):
         getattr(L, name).restype = i32
@@ -68,7 +69,7 @@ def check(status: int, what: str):
 
 # symbols include/f16env.h declares (tests check the .so exports every one of them)
 EXPORTED_SYMBOLS = (
-    "f16env_config_default", "f16env_create", "f16env_destroy", "f16env_state_bytes",
+    "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_step_kernel_name",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",

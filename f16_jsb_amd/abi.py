@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 
-F16ENV_ABI_VERSION = 1
+F16ENV_ABI_VERSION = 2
 F16_OBS_DIM = 15
 F16_ACT_DIM = 4
 
@@ -27,12 +27,15 @@ F16C_CMD = 58
 F16C_GOAL = 62
 F16C_LAST_D, F16C_STEP, F16C_EP_RET, F16C_EP_COUNT = 65, 66, 67, 68
 F16C_WIND = 69
-F16C_N = 72
+F16C_GUST = 72
+F16C_N = 75
 
 (F16L_ALPHA, F16L_BETA, F16L_MACH, F16L_VC_KTS, F16L_VG_FPS, F16L_P_AERO, F16L_Q_AERO,
  F16L_R_AERO, F16L_NPY, F16L_NPZ, F16L_N) = range(11)
 
 F16_FLAG_NO_AUTORESET = 0x1
+F16_FLAG_RANDOM_IC = 0x2  # cfg5: reset IC drawn from the [ic_lo, ic_hi] box
+F16_FLAG_GUSTS = 0x4      # cfg5: Gauss-Markov gusts on top of the steady wind
 
 # jsbsim_gym.py:28-53 observation bounds (per frame)
 EPSILON = 1e-5
@@ -53,6 +56,10 @@ class EnvConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("env_id_base", ctypes.c_int64),
         ("ic", ctypes.c_double * F16_IC_N),
+        ("ic_lo", ctypes.c_double * F16_IC_N),
+        ("ic_hi", ctypes.c_double * F16_IC_N),
+        ("gust_sigma_fps", ctypes.c_double),
+        ("gust_tau_s", ctypes.c_double),
     ]
 
 
@@ -65,7 +72,9 @@ def default_ic_values():
 
 def config_default(n_envs=1, stack_k=10, down_sample=4, max_steps=1200, flags=0,
                    dt=1.0 / 120.0, dg_m=100.0, goal_gain=1e-2, crash_alt_m=10.0, seed=0,
-                   env_id_base=0, ic=None) -> EnvConfig:
+                   env_id_base=0, ic=None, cfg5=False) -> EnvConfig:
+    """f16env_config_default with overrides; cfg5=True adds the BASELINE cfg5 random-IC box
+    and gusts (config_cfg5)."""
     c = EnvConfig()
     c.n_envs = int(n_envs)
     c.stack_k = int(stack_k)          # NUM_STACKED_FRAMES (:58)
@@ -80,7 +89,37 @@ def config_default(n_envs=1, stack_k=10, down_sample=4, max_steps=1200, flags=0,
     c.env_id_base = int(env_id_base)
     vals = default_ic_values() if ic is None else list(ic)
     for i in range(F16_IC_N):
-        c.ic[i] = float(vals[i])
+        c.ic[i] = c.ic_lo[i] = c.ic_hi[i] = float(vals[i])
+    c.gust_sigma_fps = 0.0
+    c.gust_tau_s = 2.0
+    if cfg5:
+        config_cfg5(c)
+    return c
+
+
+# BASELINE cfg5 box (include/f16env.h f16env_config_cfg5; SURVEY.md 8c cfg5 ranges)
+CFG5_BOX = {
+    F16_IC_H_SL_FT: (3000.0, 30000.0),
+    F16_IC_U_FPS: (600.0, 1200.0),
+    F16_IC_PHI_RAD: (-0.17453292519943295, 0.17453292519943295),
+    F16_IC_THETA_RAD: (-0.17453292519943295, 0.17453292519943295),
+    F16_IC_PSI_RAD: (0.0, 6.283185307179586),
+    F16_IC_CMD_THR: (0.3, 1.0),
+    F16_IC_WIND_N_FPS: (-30.0, 30.0),
+    F16_IC_WIND_E_FPS: (-30.0, 30.0),
+}
+CFG5_GUST_SIGMA_FPS = 10.0
+CFG5_GUST_TAU_S = 2.0
+
+
+def config_cfg5(c: EnvConfig) -> EnvConfig:
+    """Python twin of f16env_config_cfg5: random-IC box + gusts on top of ``c``."""
+    c.flags = int(c.flags) | F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS
+    for i in range(F16_IC_N):
+        lo, hi = CFG5_BOX.get(i, (c.ic[i], c.ic[i]))
+        c.ic_lo[i], c.ic_hi[i] = lo, hi
+    c.gust_sigma_fps = CFG5_GUST_SIGMA_FPS
+    c.gust_tau_s = CFG5_GUST_TAU_S
     return c
 
 

@@ -102,12 +102,14 @@ enum FField {
   F_GOAL = F_LX + F16L_N,
   F_LASTD = F_GOAL + 3,
   F_WIND,
-  NFF = F_WIND + 3
+  F_GUST = F_WIND + 3,  // cfg5 gust (NED fps); loaded/stored only by the gust-mode kernels
+  NFF = F_GUST + 3
 };
 enum IField { I_STEP, I_EPCOUNT, I_FLAGS, NIF };
 static constexpr int LANE_FLAG_AUG = 1;
-// persistent bytes per env (SURVEY.md 8d "S")
-static constexpr int STATE_BYTES = NDF * 8 + NFF * 4 + NIF * 4;
+// persistent bytes per env (SURVEY.md 8d "S"); the gust columns move only in gust mode
+static constexpr int STATE_BYTES = NDF * 8 + (NFF - 3) * 4 + NIF * 4;
+static constexpr int STATE_BYTES_GUST = STATE_BYTES + 12;
 
 struct SoA {
   double* d;
@@ -123,12 +125,17 @@ struct Lane {
   float pri, prp, ppi, ppp, pyi, pyp;
   float n1, n2;
   float lx[F16L_N];
-  float goal[3], last_d, wind[3];
+  float goal[3], last_d;
+  float wind[3];  // wind the FDM sees (NED fps): steady + gust
+  float wst[3];   // steady wind (SoA F_WIND); the gust-mode kernels keep it apart from
+  float gust[3];  // the cfg5 gust (SoA F_GUST)
   int32_t step, ep_count, flags;
 };
 
+template <bool GUST = false>
 __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   const int64_t n = s.n;
+
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     L.rI[j] = s.d[(D_RI0 + j) * n + k];
@@ -148,7 +155,9 @@ __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
     L.wId[j] = s.f[(F_WID + j) * n + k];
     L.ba[j] = s.f[(F_BA + j) * n + k];
     L.goal[j] = s.f[(F_GOAL + j) * n + k];
-    L.wind[j] = s.f[(F_WIND + j) * n + k];
+    L.wst[j] = s.f[(F_WIND + j) * n + k];
+    L.gust[j] = GUST ? s.f[(F_GUST + j) * n + k] : 0.0f;
+    L.wind[j] = GUST ? L.wst[j] + L.gust[j] : L.wst[j];
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) L.q[j] = s.f[(F_Q + j) * n + k];
@@ -166,8 +175,13 @@ __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   L.flags = s.i[I_FLAGS * n + k];
 }
 
+template <bool GUST = false>
 __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
   const int64_t n = s.n;
+  if (GUST) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s.f[(F_GUST + j) * n + k] = L.gust[j];
+  }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     s.d[(D_RI0 + j) * n + k] = L.rI[j];
@@ -185,7 +199,7 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
     s.f[(F_WID + j) * n + k] = L.wId[j];
     s.f[(F_BA + j) * n + k] = L.ba[j];
     s.f[(F_GOAL + j) * n + k] = L.goal[j];
-    s.f[(F_WIND + j) * n + k] = L.wind[j];
+    s.f[(F_WIND + j) * n + k] = GUST ? L.wst[j] : L.wind[j];
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) s.f[(F_Q + j) * n + k] = L.q[j];

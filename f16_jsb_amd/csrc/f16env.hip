@@ -70,6 +70,33 @@ __device__ __forceinline__ void rng_goal(uint64_t seed, uint64_t gid, uint32_t e
   g[2] = (float)alt;
 }
 
+// cfg5 random IC (include/f16env.h F16_FLAG_RANDOM_IC), mirrors oracle rng_ic()
+__device__ void rng_ic(uint64_t seed, uint64_t gid, uint32_t ep, const double* lo, const double* hi, double* ic) {
+  uint32_t o[4];
+  for (int j = 0; j < F16_IC_N; ++j) {
+    if ((j & 3) == 0)
+      philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), ep,
+             0x52494300u + (uint32_t)(j >> 2), o);
+    const double u = ((double)o[j & 3] + 0.5) * (1.0 / 4294967296.0);
+    ic[j] = lo[j] + (hi[j] - lo[j]) * u;
+  }
+}
+// cfg5 gust noise: three Box-Muller normals (fp32), mirrors oracle rng_normals() (fp64)
+__device__ __forceinline__ void rng_normals(uint64_t seed, uint64_t gid, uint32_t ep, uint32_t s, float* xi) {
+  uint32_t o[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32) ^ 0x47555354u, ep, s, o);
+  const float s24 = 1.0f / 16777216.0f;
+  const float u1 = ((float)(o[0] >> 8) + 0.5f) * s24, u2 = (float)(o[1] >> 8) * s24;
+  const float u3 = ((float)(o[2] >> 8) + 0.5f) * s24, u4 = (float)(o[3] >> 8) * s24;
+  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
+  float s2, c2, s4, c4;
+  sincospif(2.0f * u2, &s2, &c2);
+  sincospif(2.0f * u4, &s4, &c4);
+  xi[0] = r1 * c2;
+  xi[1] = r1 * s2;
+  xi[2] = r2 * c4;
+}
+
 // ------------------------------------------------------------------------------------------
 // IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
 // ------------------------------------------------------------------------------------------
@@ -131,7 +158,8 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   L.wI[2] = (float)(ic[F16_IC_R_RPS] + T8 * OMEGA_E);
   for (int j = 0; j < 3; ++j) {
     L.wId[j] = 0.0f; L.ba[j] = 0.0f; L.aI[j] = 0.0f; L.aIp[j] = 0.0f; L.dv1[j] = 0.0f; L.dv2[j] = 0.0f;
-    L.wind[j] = (float)ic[F16_IC_WIND_N_FPS + j];
+    L.wst[j] = (float)ic[F16_IC_WIND_N_FPS + j];
+    L.wind[j] = L.wst[j] + L.gust[j];  // callers set the gust (0 outside the cfg5 gust mode)
   }
   L.tef = L.ail = L.ele = L.rud = L.lef = L.sb = 0.0f;
   L.pri = L.prp = L.ppi = L.ppp = L.pyi = L.pyp = 0.0f;
@@ -195,14 +223,36 @@ struct EnvArgs {
   double gain;
   uint64_t seed;
   int64_t id_base;
+  const double* ic_cfg;  // config IC, RANDOM_IC box lo / hi (device, F16_IC_N each)
+  const double* ic_lo;
+  const double* ic_hi;
+  float gust_a, gust_b, gust_sigma;  // cfg5 Gauss-Markov gust coefficients
 };
 
-// reset a lane from the IC template (or a per-lane IC) and produce its frame 0
+// reset a lane and produce its frame 0: the IC template copy (default config), or the full
+// RunIC of a per-lane / random / config IC (cfg5 modes: the gust enters the IC passes)
 __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const float* goal,
                            const EnvArgs& E, int64_t k, const float* T, const ModelConsts& C,
                            float* f0) {
   const int32_t ep = L.ep_count;
-  if (ic) {
+  const uint64_t gid = (uint64_t)(E.id_base + k);
+  if (ic || (E.flags & (F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS))) {
+    double ric[F16_IC_N];
+    if (!ic) {
+      if (E.flags & F16_FLAG_RANDOM_IC) {
+        rng_ic(E.seed, gid, (uint32_t)ep, E.ic_lo, E.ic_hi, ric);
+        ic = ric;
+      } else {
+        ic = E.ic_cfg;
+      }
+    }
+    if (E.flags & F16_FLAG_GUSTS) {
+      float xi[3];
+      rng_normals(E.seed, gid, (uint32_t)ep, 0u, xi);
+      for (int j = 0; j < 3; ++j) L.gust[j] = E.gust_sigma * xi[j];
+    } else {
+      L.gust[0] = L.gust[1] = L.gust[2] = 0.0f;
+    }
     apply_ic(L, ic, T, C);
   } else {
     lane_load(tmpl, 0, L);
@@ -210,8 +260,20 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   if (goal) {
     L.goal[0] = goal[0]; L.goal[1] = goal[1]; L.goal[2] = goal[2];
   } else {
-    rng_goal(E.seed, (uint64_t)(E.id_base + k), (uint32_t)ep, L.goal);
+    rng_goal(E.seed, gid, (uint32_t)ep, L.goal);
   }
+  L.ep_count = ep + 1;
+  L.step = 0;
+  L.ep_ret = 0.0;
+  make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
+  L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
+}
+
+__device__ __forceinline__ void lane_reset_template(Lane& L, const SoA& tmpl, const EnvArgs& E, int64_t k,
+                                                    float* f0) {
+  const int32_t ep = L.ep_count;
+  lane_load(tmpl, 0, L);
+  rng_goal(E.seed, (uint64_t)(E.id_base + k), (uint32_t)ep, L.goal);
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
@@ -222,7 +284,9 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
+#ifndef BLOCK
 #define BLOCK 256
+#endif
 #define FRAME_PITCH 16
 
 __device__ __forceinline__ void stage_tables(float* sT) {
@@ -262,46 +326,68 @@ __device__ __forceinline__ void dma16(const float* g, float* lds) {
 // (64*KC floats) + one spare frame; fallback mode holds the final/reset frames per lane.
 __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t)64 * KC + 16; }
 
-__global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
+// MODE bit 0: F16_FLAG_RANDOM_IC, bit 1: F16_FLAG_GUSTS. MODE 0 (the reference's task) resets
+// finished lanes inline from the IC template; other modes leave finished lanes to
+// f16_reset_done_kernel (a full RunIC per lane is too long to run divergently in-wave).
+template <int MODE>
+__device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDone, float* dynl) {
+  constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
 #ifdef F16_STAMPS
   Stamps stamps = {};
   stamps.last = memtime();
 #endif
-  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
-  __shared__ int sDone[BLOCK];
-  extern __shared__ __align__(16) float dynl[];
   const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
   const int rows = (int)(a.E.n - row0 < 64 ? (a.E.n - row0 > 0 ? a.E.n - row0 : 0) : 64);
   const bool image = a.lds_image != 0;
   float* img = dynl + (size_t)wave * image_floats_per_wave(KC);
-  // 1) start the DMA of this wave's previous stack block into LDS (overlaps the physics)
-  if (image && rows > 0) {
-    const float* prev = a.obs_prev + row0 * KC;
-    const int total = rows * KC;  // floats
-    const int n16 = total >> 2;   // whole 16-byte pieces (wave blocks are 16-B aligned)
-    for (int b = 0; b < n16; b += 64) {
-      const int piece = b + lane;
-      if (piece < n16) dma16(prev + 4 * piece, img + 4 * b);
+  // 1) DMA of this wave's previous stack block into LDS (overlaps the physics)
+  auto issue_stack_dma = [&]() {
+    if (image && rows > 0) {
+      const float* prev = a.obs_prev + row0 * KC;
+      const int total = rows * KC;  // floats
+      const int n16 = total >> 2;   // whole 16-byte pieces (wave blocks are 16-B aligned)
+      for (int b = 0; b < n16; b += 64) {
+        const int piece = b + lane;
+        if (piece < n16) dma16(prev + 4 * piece, img + 4 * b);
+      }
+      if (lane < (total & 3)) img[4 * n16 + lane] = prev[4 * n16 + lane];  // tail, never past the end
     }
-    if (lane < (total & 3)) img[4 * n16 + lane] = prev[4 * n16 + lane];  // tail, never past the end
-  }
+  };
+#ifndef F16_DMA_LATE
+  issue_stack_dma();
+#endif
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = k < a.E.n;
   int done = 0;
   Lane L;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {  // issue the state loads before the table staging so their latencies overlap
-    lane_load(a.s, k, L);
+    lane_load<GUST>(a.s, k, L);
     av = reinterpret_cast<const float4*>(a.act)[k];
   }
   stage_tables(sT);
+#ifdef F16_DMA_LATE
+  // the state loads first get the full HBM bandwidth; the stack DMA then streams under the
+  // physics (it is only needed at the splice)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_stack_dma();
+#endif
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
+    if (GUST) {  // cfg5 Gauss-Markov gust update, once per env step before the frames
+      float xi[3];
+      rng_normals(a.E.seed, (uint64_t)(a.E.id_base + k), (uint32_t)(L.ep_count - 1), (uint32_t)L.step, xi);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        L.gust[j] = a.E.gust_a * L.gust[j] + a.E.gust_b * xi[j];
+        L.wind[j] = L.wst[j] + L.gust[j];
+      }
+    }
     double ce, se;
     if (fabs(L.epa) < 0.01) {  // series, exact in fp64 for |epa| < 0.01 (40 s episodes: 3e-3)
       const double e2 = L.epa * L.epa;
@@ -343,20 +429,20 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
     if (done) {
       if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
       if (a.ep_len) a.ep_len[k] = L.step;
-      if (!(a.E.flags & F16_FLAG_NO_AUTORESET)) {
-        lane_reset(L, a.tmpl, nullptr, nullptr, a.E, k, sT, a.C, f0);
+      if (!DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)) {
+        lane_reset_template(L, a.tmpl, a.E, k, f0);
       } else {
 #pragma unroll
         for (int j = 0; j < F16_OBS_DIM; ++j) f0[j] = f[j];
       }
     }
     F16_STAMP(stamps, ST_RESET);
-    lane_store(a.s, k, L);
+    lane_store<GUST>(a.s, k, L);
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
   // compaction of finished lanes (wave64 ballot)
-  if (a.done_idx) {
+  if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)
     const unsigned long long m = __ballot(done);
     int base = 0;
     if (m) {
@@ -365,7 +451,8 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
       if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
     }
   }
-  const bool autoreset = !(a.E.flags & F16_FLAG_NO_AUTORESET);
+  // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel
+  const bool autoreset = !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET);
   if (image) {
     // 2) splice the new frame of row r into the image at row r+1's first frame, which the
     //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block
@@ -467,6 +554,50 @@ __global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
 #endif
 }
 
+#define STEP_SHARED                                       \
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];   \
+  __shared__ int sDone[BLOCK];                            \
+  extern __shared__ __align__(16) float dynl[];
+
+__global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
+  STEP_SHARED
+  step_body<0>(a, sT, sDone, dynl);
+}
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void f16_step_cfg5_kernel(StepArgs a) {
+  STEP_SHARED
+  step_body<MODE>(a, sT, sDone, dynl);
+}
+
+// cfg5 auto-reset of the lanes a deferred-mode step finished (done list from its ballot
+// compaction): full RunIC (random IC box, gust start) and K x frame 0 into their obs rows.
+struct ResetDoneArgs {
+  SoA s, tmpl;
+  const int32_t* done_idx;
+  const int32_t* n_done;
+  float* obs;
+  EnvArgs E;
+  ModelConsts C;
+};
+__global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) {
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
+  const int nd = *a.n_done;
+  if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // block-uniform: no barrier skipped by part of a block
+  stage_tables(sT);
+  for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < nd; i += (int64_t)gridDim.x * BLOCK) {
+    const int64_t k = a.done_idx[i];
+    if (k < 0 || k >= a.E.n) continue;
+    Lane L;
+    lane_load<true>(a.s, k, L);
+    float f0[F16_OBS_DIM];
+    lane_reset(L, a.tmpl, nullptr, nullptr, a.E, k, sT, a.C, f0);
+    lane_store<true>(a.s, k, L);
+    float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;
+    for (int r = 0; r < a.E.K; ++r)
+      for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
+  }
+}
+
 struct ResetArgs {
   SoA s, tmpl;
   const uint8_t* mask;
@@ -483,11 +614,11 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   if (k >= a.E.n) return;
   if (a.mask && !a.mask[k]) return;
   Lane L;
-  lane_load(a.s, k, L);
+  lane_load<true>(a.s, k, L);
   float f0[F16_OBS_DIM];
   lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, a.goals ? a.goals + 3 * k : nullptr,
              a.E, k, sT, a.C, f0);
-  lane_store(a.s, k, L);
+  lane_store<true>(a.s, k, L);
   if (a.obs) {
     float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;
     for (int r = 0; r < a.E.K; ++r)
@@ -512,7 +643,7 @@ __global__ void f16_get_state_kernel(SoA s, double* c) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= s.n) return;
   Lane L;
-  lane_load(s, k, L);
+  lane_load<true>(s, k, L);
   double* o = c + (int64_t)F16C_N * k;
   for (int j = 0; j < 3; ++j) {
     o[F16C_RI + j] = L.rI[j]; o[F16C_VI + j] = L.vI[j];
@@ -520,7 +651,8 @@ __global__ void f16_get_state_kernel(SoA s, double* c) {
     o[F16C_VIH2 + j] = L.vI[j] + (double)L.dv2[j];
     o[F16C_AI + j] = L.aI[j]; o[F16C_AIP + j] = L.aIp[j]; o[F16C_WI + j] = L.wI[j];
     o[F16C_WID + j] = L.wId[j]; o[F16C_BA + j] = L.ba[j]; o[F16C_GOAL + j] = L.goal[j];
-    o[F16C_WIND + j] = L.wind[j];
+    o[F16C_WIND + j] = L.wst[j];
+    o[F16C_GUST + j] = L.gust[j];
   }
   for (int j = 0; j < 4; ++j) { o[F16C_Q + j] = L.q[j]; o[F16C_CMD + j] = 0.0; }
   o[F16C_EPA_C] = cos(L.epa); o[F16C_EPA_S] = sin(L.epa);
@@ -545,7 +677,9 @@ __global__ void f16_set_state_kernel(SoA s, const double* c) {
     L.dv2[j] = (float)(o[F16C_VIH2 + j] - o[F16C_VI + j]);
     L.aI[j] = (float)o[F16C_AI + j]; L.aIp[j] = (float)o[F16C_AIP + j]; L.wI[j] = (float)o[F16C_WI + j];
     L.wId[j] = (float)o[F16C_WID + j]; L.ba[j] = (float)o[F16C_BA + j]; L.goal[j] = (float)o[F16C_GOAL + j];
-    L.wind[j] = (float)o[F16C_WIND + j];
+    L.wst[j] = (float)o[F16C_WIND + j];
+    L.gust[j] = (float)o[F16C_GUST + j];
+    L.wind[j] = L.wst[j] + L.gust[j];
   }
   for (int j = 0; j < 4; ++j) L.q[j] = (float)o[F16C_Q + j];
   L.epa = atan2(o[F16C_EPA_S], o[F16C_EPA_C]);
@@ -558,7 +692,7 @@ __global__ void f16_set_state_kernel(SoA s, const double* c) {
   for (int j = 0; j < F16L_N; ++j) L.lx[j] = (float)o[F16C_LX + j];
   L.last_d = (float)o[F16C_LAST_D]; L.step = (int32_t)o[F16C_STEP]; L.ep_ret = o[F16C_EP_RET];
   L.ep_count = (int32_t)(uint32_t)o[F16C_EP_COUNT];
-  lane_store(s, k, L);
+  lane_store<true>(s, k, L);
 }
 
 // Trim: Newton on (alpha, elevator cmd, throttle cmd), mirrors oracle trim_one()
@@ -577,6 +711,7 @@ __device__ void trim_residual(const double* icb, const float* x, const float* T,
   ic[F16_IC_CMD_ELE] = x[1];
   ic[F16_IC_CMD_THR] = x[2];
   Lane L;
+  L.gust[0] = L.gust[1] = L.gust[2] = 0.0f;
   apply_ic(L, ic, T, C);
   // FGAccelerations::CalculateUVWdot: specific force + gravity - (pqr + 2 w_b) x uvw
   // - Ti2b (w x (w x rI))
@@ -707,7 +842,9 @@ struct f16env {
   int device;
   void* mem;       // state SoA
   void* tmem;      // template SoA (n = 1)
-  double* ic_dev;  // default IC
+  double* ic_dev;  // default IC, RANDOM_IC box lo, hi (3 x F16_IC_N)
+  int32_t* done_buf;  // deferred modes: own done list (N) + count, when the caller gives none
+  int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 GUSTS
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
@@ -793,6 +930,14 @@ static EnvArgs env_args(const f16env* h) {
   E.gain = h->cfg.goal_gain;
   E.seed = h->cfg.seed;
   E.id_base = h->cfg.env_id_base;
+  E.ic_cfg = h->ic_dev;
+  E.ic_lo = h->ic_dev + F16_IC_N;
+  E.ic_hi = h->ic_dev + 2 * F16_IC_N;
+  // a = exp(-T/tau), b = sigma sqrt(1 - a^2) over the env step T = down_sample dt (oracle gust_coeffs)
+  const double ga = h->cfg.gust_tau_s > 0.0 ? exp(-(double)h->cfg.down_sample * h->cfg.dt / h->cfg.gust_tau_s) : 0.0;
+  E.gust_a = (float)ga;
+  E.gust_b = (float)(h->cfg.gust_sigma_fps * sqrt(1.0 - ga * ga));
+  E.gust_sigma = (float)h->cfg.gust_sigma_fps;
   return E;
 }
 
@@ -811,6 +956,27 @@ int f16env_config_default(f16env_config* c) {
   c->crash_alt_m = 10.0;
   c->ic[F16_IC_H_SL_FT] = 5000.0;
   c->ic[F16_IC_U_FPS] = 900.0;
+  for (int j = 0; j < F16_IC_N; ++j) c->ic_lo[j] = c->ic_hi[j] = c->ic[j];
+  c->gust_sigma_fps = 0.0;
+  c->gust_tau_s = 2.0;
+  return 0;
+}
+
+int f16env_config_cfg5(f16env_config* c) {
+  if (!c) return set_err(-1, "null config");
+  c->flags |= F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS;
+  for (int j = 0; j < F16_IC_N; ++j) c->ic_lo[j] = c->ic_hi[j] = c->ic[j];
+  const double deg10 = 0.17453292519943295;
+  c->ic_lo[F16_IC_H_SL_FT] = 3000.0;  c->ic_hi[F16_IC_H_SL_FT] = 30000.0;
+  c->ic_lo[F16_IC_U_FPS] = 600.0;     c->ic_hi[F16_IC_U_FPS] = 1200.0;
+  c->ic_lo[F16_IC_PHI_RAD] = -deg10;  c->ic_hi[F16_IC_PHI_RAD] = deg10;
+  c->ic_lo[F16_IC_THETA_RAD] = -deg10; c->ic_hi[F16_IC_THETA_RAD] = deg10;
+  c->ic_lo[F16_IC_PSI_RAD] = 0.0;     c->ic_hi[F16_IC_PSI_RAD] = 6.283185307179586;
+  c->ic_lo[F16_IC_CMD_THR] = 0.3;     c->ic_hi[F16_IC_CMD_THR] = 1.0;
+  c->ic_lo[F16_IC_WIND_N_FPS] = -30.0; c->ic_hi[F16_IC_WIND_N_FPS] = 30.0;
+  c->ic_lo[F16_IC_WIND_E_FPS] = -30.0; c->ic_hi[F16_IC_WIND_E_FPS] = 30.0;
+  c->gust_sigma_fps = 10.0;
+  c->gust_tau_s = 2.0;
   return 0;
 }
 
@@ -820,6 +986,8 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   if (cfg->stack_k < 1 || cfg->stack_k > 64) return set_err(-1, "stack_k must be in [1, 64]");
   if (cfg->down_sample < 0) return set_err(-1, "down_sample must be >= 0");
   if (!(cfg->dt > 0.0)) return set_err(-1, "dt must be > 0");
+  if ((cfg->flags & F16_FLAG_GUSTS) && !(cfg->gust_sigma_fps >= 0.0 && cfg->gust_tau_s > 0.0))
+    return set_err(-1, "gusts need gust_sigma_fps >= 0 and gust_tau_s > 0");
   HIPCHK(hipSetDevice(device));
   f16env* h = new f16env();
   h->cfg = *cfg;
@@ -830,8 +998,12 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   if (e != hipSuccess) { delete h; return set_err(-3, "hipMalloc(state) failed"); }
   hipMemset(h->mem, 0, h->bytes);
   soa_carve(h->mem, cfg->n_envs, h->soa);
-  if (hipMalloc(&h->tmem, soa_bytes(1)) != hipSuccess || hipMalloc((void**)&h->ic_dev, sizeof(double) * F16_IC_N) != hipSuccess) {
-    hipFree(h->mem); delete h;
+  h->mode = ((cfg->flags & F16_FLAG_RANDOM_IC) ? 1 : 0) | ((cfg->flags & F16_FLAG_GUSTS) ? 2 : 0);
+  h->done_buf = nullptr;
+  if (hipMalloc(&h->tmem, soa_bytes(1)) != hipSuccess ||
+      hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||
+      (h->mode && hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 1)) != hipSuccess)) {
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
     return set_err(-3, "hipMalloc(template) failed");
   }
   soa_carve(h->tmem, 1, h->tmpl);
@@ -843,13 +1015,18 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : 0;
     h->dyn_lds = h->lds_image ? img : fallback;
     hipFuncSetAttribute((const void*)f16_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
+    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
+    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
+    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
   }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
+  hipMemcpy(h->ic_dev + F16_IC_N, cfg->ic_lo, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
+  hipMemcpy(h->ic_dev + 2 * F16_IC_N, cfg->ic_hi, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipLaunchKernelGGL(f16_ic_kernel, dim3(1), dim3(BLOCK), 0, 0, h->tmpl, (const double*)h->ic_dev, h->C);
   e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) {
-    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
     return set_err(-2, hipGetErrorString(e));
   }
   *out = h;
@@ -862,6 +1039,7 @@ int f16env_destroy(f16env_t h) {
   hipFree(h->mem);
   hipFree(h->tmem);
   hipFree(h->ic_dev);
+  if (h->done_buf) hipFree(h->done_buf);
   delete h;
   return 0;
 }
@@ -899,9 +1077,28 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
   a.lds_image = h->lds_image;
   if (((uintptr_t)obs & 15) != 0 || ((uintptr_t)obs_prev & 15) != 0)
     return set_err(-1, "obs and obs_prev must be 16-byte aligned");
-  if (n_done) HIPCHK(hipMemsetAsync(n_done, 0, sizeof(int32_t), (hipStream_t)stream));
-  hipLaunchKernelGGL(f16_step_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), h->dyn_lds, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  if (h->mode && !done_idx) {  // deferred resets need the done list
+    a.done_idx = h->done_buf;
+    a.n_done = h->done_buf + h->cfg.n_envs;
+  }
+  if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
+  const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
+  switch (h->mode) {
+    case 0: hipLaunchKernelGGL(f16_step_kernel, grid, blk, h->dyn_lds, st, a); break;
+    case 1: hipLaunchKernelGGL(f16_step_cfg5_kernel<1>, grid, blk, h->dyn_lds, st, a); break;
+    case 2: hipLaunchKernelGGL(f16_step_cfg5_kernel<2>, grid, blk, h->dyn_lds, st, a); break;
+    default: hipLaunchKernelGGL(f16_step_cfg5_kernel<3>, grid, blk, h->dyn_lds, st, a); break;
+  }
   HIPCHK(hipGetLastError());
+  if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
+    ResetDoneArgs r;
+    r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = obs;
+    r.E = a.E; r.C = h->C;
+    const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
+    hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
+    HIPCHK(hipGetLastError());
+  }
   return 0;
 }
 

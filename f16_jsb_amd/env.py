@@ -60,7 +60,7 @@ class F16Envs:
             raise F16EnvError("device must be a cuda (ROCm) device, got %s" % self.device)
         self.n = int(n_envs)
         self.k = int(stack_k)
-        flags = 0 if autoreset else F16_FLAG_NO_AUTORESET
+        flags = int(cfg_kw.pop("flags", 0)) | (0 if autoreset else F16_FLAG_NO_AUTORESET)
         self.cfg: EnvConfig = config_default(n_envs=n_envs, stack_k=stack_k, seed=seed, env_id_base=env_id_base,
                                              max_steps=max_steps, down_sample=down_sample, flags=flags, ic=ic,
                                              **cfg_kw)
@@ -123,9 +123,11 @@ class F16Envs:
         check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
         return out
 
-    def step(self, actions) -> StepOut:
+    def step(self, actions, done_idx=None, n_done=None) -> StepOut:
         """One env step for all lanes; ``actions`` (N,4) float32 device tensor (or host
-        array, copied). Returns device tensors; obs alternates between two buffers."""
+        array, copied). Returns device tensors; obs alternates between two buffers.
+        done_idx (N,) / n_done (1,) int32 device tensors receive the compacted list of lanes
+        that finished (optional)."""
         t = self.torch
         if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
                 and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
@@ -139,7 +141,7 @@ class F16Envs:
         nxt = self._obs[self._cur ^ 1]
         check(lib().f16env_step(self._h, self._stream(), _ptr(act), _ptr(prev), _ptr(nxt), _ptr(self.rew),
                                 _ptr(self.term), _ptr(self.trunc), _ptr(self.terminal_obs),
-                                _ptr(self.ep_return), _ptr(self.ep_len), None, None), "f16env_step")
+                                _ptr(self.ep_return), _ptr(self.ep_len), _ptr(done_idx), _ptr(n_done)), "f16env_step")
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 

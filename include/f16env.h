@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define F16ENV_ABI_VERSION 1
+#define F16ENV_ABI_VERSION 2
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
 #define F16_OBS_DIM 15
@@ -102,7 +102,8 @@ enum f16_canon_index {
   F16C_EP_RET = 67,  /* Monitor episode return (sum of float64 rewards)                */
   F16C_EP_COUNT = 68,/* resets so far (keys the device goal RNG)                        */
   F16C_WIND = 69,    /* 69-71 steady wind NED (fps)                                     */
-  F16C_N = 72
+  F16C_GUST = 72,    /* 72-74 gust wind NED (fps), F16_FLAG_GUSTS (cfg5)                  */
+  F16C_N = 75
 };
 enum f16_latch_index {
   F16L_ALPHA = 0, F16L_BETA, F16L_MACH, F16L_VC_KTS, F16L_VG_FPS,
@@ -111,6 +112,17 @@ enum f16_latch_index {
 
 /* flags */
 #define F16_FLAG_NO_AUTORESET 0x1 /* leave done lanes un-reset (caller resets)          */
+/* BASELINE cfg5 (the reference has neither: it always resets to jsbsim_gym.py:166-170 and
+ * never enables FGWinds). Build-defined models, documented in DESIGN.md:
+ *   RANDOM_IC: every reset that is not given an explicit IC (auto-reset, f16env_reset with
+ *     ic == NULL) draws ic[j] = ic_lo[j] + (ic_hi[j] - ic_lo[j]) * u_j, u_j = (w_j + 0.5) 2^-32,
+ *     w_j word j of Philox4x32-10 keyed by (seed; gid, gid_hi, episode, 0x52494300 + j/4).
+ *   GUSTS: per-lane first-order Gauss-Markov gust g (NED, fps) added to the steady wind:
+ *     g_0 = sigma * xi_0 at reset, g_s = a g_{s-1} + sigma sqrt(1 - a^2) xi_s before the FDM
+ *     frames of env step s, a = exp(-down_sample dt / tau); xi_s three Box-Muller normals
+ *     from Philox keyed by (seed; gid, gid_hi ^ 0x47555354, episode, s). */
+#define F16_FLAG_RANDOM_IC 0x2
+#define F16_FLAG_GUSTS 0x4
 
 typedef struct f16env_config {
   int32_t n_envs;       /* envs on this device                                          */
@@ -126,12 +138,21 @@ typedef struct f16env_config {
   uint64_t seed;        /* device RNG seed for auto-reset goals                          */
   int64_t env_id_base;  /* global id of local env 0 (multi-GPU shards key the RNG by it) */
   double ic[F16_IC_N];  /* default initial condition                                    */
+  double ic_lo[F16_IC_N]; /* F16_FLAG_RANDOM_IC box, per IC component (lo == hi: fixed)    */
+  double ic_hi[F16_IC_N];
+  double gust_sigma_fps;  /* F16_FLAG_GUSTS: stationary std-dev per NED axis              */
+  double gust_tau_s;      /*                 correlation time                              */
 } f16env_config;
 
 typedef struct f16env* f16env_t;
 
 /* Fill *cfg with the reference's defaults (n_envs=1, K=10, down_sample=4, ...). */
 int f16env_config_default(f16env_config* cfg);
+/* BASELINE cfg5 on top of *cfg: sets F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS and the build's
+ * box (u 600..1200 fps, h 3000..30000 ft, psi 0..2pi, theta/phi +-10 deg, steady wind N/E
+ * +-30 fps, throttle cmd 0.3..1) and gusts (sigma 10 fps, tau 2 s); other components
+ * keep cfg->ic. */
+int f16env_config_cfg5(f16env_config* cfg);
 
 /* Create a handle on `device`; allocates the SoA state (no per-step allocation later). */
 int f16env_create(const f16env_config* cfg, int device, f16env_t* out);

@@ -389,6 +389,7 @@ typedef struct {
   double lx[F16L_N];
   double cmd[4];
   double wind[3];
+  double gust[3]; /* cfg5 Gauss-Markov gust, NED fps (F16_FLAG_GUSTS) */
   float goal[3];
   float last_d;
   int32_t step;
@@ -693,8 +694,8 @@ static void frame(env_t* e, double dt, int ic, frame_diag_t* diag) {
   fcs_out_t fc;
   fcs_run(e, &d, dt, ic, &fc);
   /* Auxiliary */
-  double wb[3];
-  mv(d.Tl2b, e->wind, wb);
+  double wb[3], wt[3] = {e->wind[0] + e->gust[0], e->wind[1] + e->gust[1], e->wind[2] + e->gust[2]};
+  mv(d.Tl2b, wt, wb);
   double ua = d.uvw[0] - wb[0], va = d.uvw[1] - wb[1], wa = d.uvw[2] - wb[2];
   double vt = sqrt(ua * ua + va * va + wa * wa);
   double muw = ua * ua + wa * wa;
@@ -899,11 +900,57 @@ static void rng_goal(uint64_t seed, uint64_t gid, uint64_t ep, float* g) {
   g[2] = (float)alt;
 }
 
+/* cfg5 random IC (include/f16env.h F16_FLAG_RANDOM_IC): component j uniform in
+ * [lo_j, hi_j] from word j%4 of Philox (seed; gid, gid_hi, ep, 'RIC'+j/4) */
+static void rng_ic(uint64_t seed, uint64_t gid, uint64_t ep, const double* lo, const double* hi, double* ic) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t o[4];
+  for (int j = 0; j < F16_IC_N; j++) {
+    if ((j & 3) == 0) {
+      uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)ep, 0x52494300u + (uint32_t)(j >> 2)};
+      f16ref_philox4x32(key, ctr, o);
+    }
+    double u = ((double)o[j & 3] + 0.5) * (1.0 / 4294967296.0);
+    ic[j] = lo[j] + (hi[j] - lo[j]) * u;
+  }
+}
+/* cfg5 gust noise: three Box-Muller normals from Philox (seed; gid, gid_hi ^ 'GUST', ep, s) */
+static void rng_normals(uint64_t seed, uint64_t gid, uint64_t ep, uint32_t s, double* xi) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32) ^ 0x47555354u, (uint32_t)ep, s};
+  uint32_t o[4];
+  f16ref_philox4x32(key, ctr, o);
+  const double s24 = 1.0 / 16777216.0;
+  double u1 = ((double)(o[0] >> 8) + 0.5) * s24, u2 = (double)(o[1] >> 8) * s24;
+  double u3 = ((double)(o[2] >> 8) + 0.5) * s24, u4 = (double)(o[3] >> 8) * s24;
+  double r1 = sqrt(-2.0 * log(u1)), r2 = sqrt(-2.0 * log(u3));
+  xi[0] = r1 * cos(2.0 * PI * u2);
+  xi[1] = r1 * sin(2.0 * PI * u2);
+  xi[2] = r2 * cos(2.0 * PI * u4);
+}
+static void gust_coeffs(const f16env_config* c, double* a, double* b) {
+  *a = c->gust_tau_s > 0.0 ? exp(-(double)c->down_sample * c->dt / c->gust_tau_s) : 0.0;
+  *b = c->gust_sigma_fps * sqrt(1.0 - *a * *a);
+}
+
 static void env_reset(f16ref* h, int i, const float* goal, const double* ic) {
   env_t* e = &h->env[i];
+  const uint64_t gid = (uint64_t)(h->cfg.env_id_base + i);
+  double ric[F16_IC_N];
+  if (!ic && (h->cfg.flags & F16_FLAG_RANDOM_IC)) {
+    rng_ic(h->cfg.seed, gid, e->ep_count, h->cfg.ic_lo, h->cfg.ic_hi, ric);
+    ic = ric;
+  }
+  if (h->cfg.flags & F16_FLAG_GUSTS) { /* stationary start g_0 = sigma xi_0 */
+    double xi[3];
+    rng_normals(h->cfg.seed, gid, e->ep_count, 0u, xi);
+    for (int k = 0; k < 3; k++) e->gust[k] = h->cfg.gust_sigma_fps * xi[k];
+  } else {
+    e->gust[0] = e->gust[1] = e->gust[2] = 0.0;
+  }
   apply_ic(e, ic ? ic : h->cfg.ic, h->cfg.dt);
   if (goal) { e->goal[0] = goal[0]; e->goal[1] = goal[1]; e->goal[2] = goal[2]; }
-  else rng_goal(h->cfg.seed, (uint64_t)(h->cfg.env_id_base + i), e->ep_count, e->goal);
+  else rng_goal(h->cfg.seed, gid, e->ep_count, e->goal);
   e->ep_count += 1;
   e->step = 0;
   e->ep_ret = 0.0;
@@ -968,6 +1015,12 @@ int f16ref_step(f16ref* h, const float* act, float* obs, float* rew, uint8_t* te
     env_t* e = &h->env[i];
     e->step += 1;                                                   /* :215 */
     for (int j = 0; j < 4; j++) e->cmd[j] = (double)act[4 * i + j]; /* :219-222 */
+    if (h->cfg.flags & F16_FLAG_GUSTS) {                            /* cfg5 gust update */
+      double xi[3], ga, gb;
+      gust_coeffs(&h->cfg, &ga, &gb);
+      rng_normals(h->cfg.seed, (uint64_t)(h->cfg.env_id_base + i), e->ep_count - 1, (uint32_t)e->step, xi);
+      for (int k = 0; k < 3; k++) e->gust[k] = ga * e->gust[k] + gb * xi[k];
+    }
     for (int s = 0; s < h->cfg.down_sample; s++) frame(e, dt, 0, NULL); /* :225-232 */
     float f[F16_OBS_DIM];
     make_frame(e, f);                                               /* :234 */
@@ -1017,7 +1070,7 @@ int f16ref_get_state(const f16ref* h, double* c) {
       s[F16C_RI + k] = e->rI[k]; s[F16C_VI + k] = e->vI[k]; s[F16C_VIH1 + k] = e->vIh1[k];
       s[F16C_VIH2 + k] = e->vIh2[k]; s[F16C_AI + k] = e->aI[k]; s[F16C_AIP + k] = e->aIp[k];
       s[F16C_WI + k] = e->wI[k]; s[F16C_WID + k] = e->wId[k]; s[F16C_BA + k] = e->ba[k];
-      s[F16C_GOAL + k] = e->goal[k]; s[F16C_WIND + k] = e->wind[k];
+      s[F16C_GOAL + k] = e->goal[k]; s[F16C_WIND + k] = e->wind[k]; s[F16C_GUST + k] = e->gust[k];
     }
     for (int k = 0; k < 4; k++) { s[F16C_Q + k] = e->q[k]; s[F16C_CMD + k] = e->cmd[k]; }
     s[F16C_EPA_C] = e->epa_c; s[F16C_EPA_S] = e->epa_s;
@@ -1041,7 +1094,7 @@ int f16ref_set_state(f16ref* h, const double* c) {
       e->rI[k] = s[F16C_RI + k]; e->vI[k] = s[F16C_VI + k]; e->vIh1[k] = s[F16C_VIH1 + k];
       e->vIh2[k] = s[F16C_VIH2 + k]; e->aI[k] = s[F16C_AI + k]; e->aIp[k] = s[F16C_AIP + k];
       e->wI[k] = s[F16C_WI + k]; e->wId[k] = s[F16C_WID + k]; e->ba[k] = s[F16C_BA + k];
-      e->goal[k] = (float)s[F16C_GOAL + k]; e->wind[k] = s[F16C_WIND + k];
+      e->goal[k] = (float)s[F16C_GOAL + k]; e->wind[k] = s[F16C_WIND + k]; e->gust[k] = s[F16C_GUST + k];
     }
     for (int k = 0; k < 4; k++) { e->q[k] = s[F16C_Q + k]; e->cmd[k] = s[F16C_CMD + k]; }
     e->epa_c = s[F16C_EPA_C]; e->epa_s = s[F16C_EPA_S];

@@ -55,8 +55,8 @@ def test_config_default_matches_python_mirror(so_path):
     p = config_default()
     for f, _ in EnvConfig._fields_:
         a, b = getattr(c, f), getattr(p, f)
-        if f == "ic":
-            assert list(a) == list(b)
+        if f in ("ic", "ic_lo", "ic_hi"):
+            assert list(a) == list(b), f
         else:
             assert a == b, f
 
@@ -66,10 +66,12 @@ def test_header_enums_match_python_mirror():
     src = open(HDR).read()
     for name, val in re.findall(r"\b(F16C_\w+)\s*=\s*(\d+)", src):
         assert getattr(abi, name) == int(val), name
-    ic_names = re.findall(r"\b(F16_IC_\w+)\s*[,=]", src)
-    for i, name in enumerate(n for n in ic_names if n != "F16_IC_LAT_GEOD_RAD" or True):
-        pass
-    assert abi.F16_IC_N == 19 and abi.F16C_N == 72
+    ic_names = re.findall(r"^\s+(F16_IC_\w+)\s*[,=]", src, re.M)
+    assert [getattr(abi, n) for n in ic_names] == list(range(len(ic_names)))
+    for name, val in re.findall(r"#define (F16_FLAG_\w+)\s+(0x[0-9a-fA-F]+)", src):
+        assert getattr(abi, name) == int(val, 16), name
+    assert f"#define F16ENV_ABI_VERSION {abi.F16ENV_ABI_VERSION}" in src
+    assert abi.F16_IC_N == 19 and abi.F16C_N == 75
     assert "#define F16_OBS_DIM 15" in src
 
 
