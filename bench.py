@@ -190,6 +190,7 @@ def main():
     venv = F16VecEnv(num_envs=n, stack_k=args.stack, device=dev, seed=args.seed, return_numpy=False,
                      env_id_base=rank * n, cfg5=cfg5)
     envs = venv.envs
+    kernel_name, waves_per_simd = envs.step_kernel_name, envs.waves_per_simd
     venv.reset()
     pool = args.action_pool if args.action_pool > 0 else args.steps
     acts = torch.empty((pool, n, 4), dtype=torch.float32, device=dev)
@@ -286,7 +287,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
-            "kernel": "f16_step_cfg5_kernel<3> + f16_reset_done_kernel" if cfg5 else "f16_step_kernel",
+            "kernel": kernel_name + (" + f16_reset_done_kernel" if cfg5 else ""),
+            "waves_per_simd": waves_per_simd,
             "kernel_ms": round(gpu_ms_per_step, 5),
             "kernel_timing": "HIP events around the timed region on the launch stream / launches",
             "kernel_ms_event_pair_median": round(kern_ms, 5),

@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -559,14 +560,25 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
   __shared__ int sDone[BLOCK];                            \
   extern __shared__ __align__(16) float dynl[];
 
-__global__ __launch_bounds__(BLOCK) void f16_step_kernel(StepArgs a) {
+// Occupancy variants. The body needs ~300 registers (VGPR + AGPR), i.e. one wave per SIMD;
+// OCC = 2 caps it at 256 (a few spills) so two waves share each SIMD: slower per wave, but
+// when there are more waves than SIMDs (N > 64 x 4 x CUs) the pair overlaps one wave's
+// memory phases and stalls with the other's VALU work (f16env_step picks per launch).
+__global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(StepArgs a) {
   STEP_SHARED
   step_body<0>(a, sT, sDone, dynl);
 }
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) void f16_step_cfg5_kernel(StepArgs a) {
+template <int MODE, int OCC>
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
   STEP_SHARED
   step_body<MODE>(a, sT, sDone, dynl);
+}
+using StepKernel = void (*)(StepArgs);
+static StepKernel step_kernel_for(int mode, int occ) {
+  static const StepKernel table[2][4] = {
+      {f16_step_kernel, f16_step_var_kernel<1, 1>, f16_step_var_kernel<2, 1>, f16_step_var_kernel<3, 1>},
+      {f16_step_var_kernel<0, 2>, f16_step_var_kernel<1, 2>, f16_step_var_kernel<2, 2>, f16_step_var_kernel<3, 2>}};
+  return table[occ == 2 ? 1 : 0][mode & 3];
 }
 
 // cfg5 auto-reset of the lanes a deferred-mode step finished (done list from its ballot
@@ -845,6 +857,7 @@ struct f16env {
   double* ic_dev;  // default IC, RANDOM_IC box lo, hi (3 x F16_IC_N)
   int32_t* done_buf;  // deferred modes: own done list (N) + count, when the caller gives none
   int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 GUSTS
+  int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
@@ -1014,10 +1027,18 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + sizeof(int) * BLOCK + 64;
     h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : 0;
     h->dyn_lds = h->lds_image ? img : fallback;
-    hipFuncSetAttribute((const void*)f16_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
-    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
-    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
-    hipFuncSetAttribute((const void*)f16_step_cfg5_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->dyn_lds);
+    for (int occ = 1; occ <= 2; ++occ)
+      for (int m = 0; m < 4; ++m)
+        hipFuncSetAttribute((const void*)step_kernel_for(m, occ), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)h->dyn_lds);
+    // two waves per SIMD only pay when there are more waves than SIMDs and two workgroups'
+    // LDS (tables + stack image) fit in one CU
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int64_t waves = ((int64_t)cfg->n_envs + 63) / 64;
+    h->occ = (waves > 4 * (int64_t)cus && 2 * (static_lds + h->dyn_lds) <= 160 * 1024) ? 2 : 1;
+    if (getenv("F16ENV_OCC")) h->occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
   }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + F16_IC_N, cfg->ic_lo, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
@@ -1084,12 +1105,7 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
   }
   if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  switch (h->mode) {
-    case 0: hipLaunchKernelGGL(f16_step_kernel, grid, blk, h->dyn_lds, st, a); break;
-    case 1: hipLaunchKernelGGL(f16_step_cfg5_kernel<1>, grid, blk, h->dyn_lds, st, a); break;
-    case 2: hipLaunchKernelGGL(f16_step_cfg5_kernel<2>, grid, blk, h->dyn_lds, st, a); break;
-    default: hipLaunchKernelGGL(f16_step_cfg5_kernel<3>, grid, blk, h->dyn_lds, st, a); break;
-  }
+  hipLaunchKernelGGL(step_kernel_for(h->mode, h->occ), grid, blk, h->dyn_lds, st, a);
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
@@ -1147,6 +1163,7 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
 }
 
 const char* f16env_step_kernel_name(void) { return "f16_step_kernel"; }
+int f16env_step_waves_per_simd(f16env_t h) { return h ? h->occ : 0; }
 
 double f16env_algorithmic_bytes_per_env_step(int stack_k) {
   return 16.0 + 60.0 * stack_k + 60.0 * (stack_k - 1) + 4.0 + 2.0 + 2.0 * STATE_BYTES;

@@ -21,8 +21,8 @@ import numpy as np
 
 from . import spaces
 from ._lib import F16EnvError, check, lib
-from .abi import (F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_NO_AUTORESET, EnvConfig,
-                  algorithmic_bytes_per_env_step, config_default)
+from .abi import (F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC,
+                  EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
 StepOut = namedtuple("StepOut", "obs rew terminated truncated terminal_obs ep_return ep_len")
 
@@ -99,6 +99,17 @@ class F16Envs:
             self.close()
         except Exception:
             pass
+
+    @property
+    def waves_per_simd(self) -> int:
+        """Occupancy the step kernel variant of this handle is built for (1 or 2)."""
+        return int(lib().f16env_step_waves_per_simd(self._h))
+
+    @property
+    def step_kernel_name(self) -> str:
+        mode = (1 if self.cfg.flags & F16_FLAG_RANDOM_IC else 0) | (2 if self.cfg.flags & F16_FLAG_GUSTS else 0)
+        occ = self.waves_per_simd
+        return "f16_step_kernel" if (mode, occ) == (0, 1) else "f16_step_var_kernel<%d, %d>" % (mode, occ)
 
     @property
     def state_bytes_per_env(self) -> int:

@@ -209,6 +209,9 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
 /* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
  * HBM bytes one env-step moves. */
 const char* f16env_step_kernel_name(void);
+/* Waves per SIMD the handle's step kernel is built for: 1 (up to 64 x 4 x CUs envs), or 2
+ * when there are more waves than SIMDs (override: env F16ENV_OCC=1|2 at create). */
+int f16env_step_waves_per_simd(f16env_t h);
 double f16env_algorithmic_bytes_per_env_step(int stack_k);
 
 const char* f16env_last_error(void);

@@ -73,3 +73,24 @@ def test_rollout_buffer_rebuilds_env_observations(gpu):
     assert int(buf.episode_starts[1:].sum().item()) > 0, "expected auto-resets in the rollout"
     rebuilt = buf.observations()
     assert torch.equal(rebuilt, torch.stack(seen))
+
+
+def test_two_wave_variant_matches_one_wave_variant(gpu, monkeypatch):
+    """The occupancy-2 build of the step kernel (picked above 64 x 4 x CUs envs) computes
+    the same results as the one-wave build: forced on a small batch via F16ENV_OCC."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    n = 2048
+    outs = []
+    for occ in ("1", "2"):
+        monkeypatch.setenv("F16ENV_OCC", occ)
+        e = F16Envs(n, stack_k=4, seed=9)
+        assert e.waves_per_simd == int(occ)
+        e.reset()
+        for t in range(40):
+            o = e.step(e.sample_actions(4, t))
+        outs.append((o.obs.clone(), o.rew.clone(), e.get_state()))
+        e.close()
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=0, atol=0)
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=0, atol=0)
