@@ -148,13 +148,14 @@ def rollout_bench(args, dev, rank, world):
     return r
 
 
-def load_traffic(envs, stack):
-    """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if present."""
+def load_traffic(envs, stack, state_bytes):
+    """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if it was
+    measured on this workload and state layout."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("envs") == envs and d.get("stack_k") == stack:
+        if d.get("envs") == envs and d.get("stack_k") == stack and d.get("state_bytes") == state_bytes:
             return d.get("hbm_bytes_per_launch")
     except Exception:  # noqa: BLE001
         pass
@@ -254,7 +255,7 @@ def main():
     # bounds the rocprof kernel duration from above). The per-launch event median (which also
     # counts event overhead) is reported beside it.
     achieved = bytes_per_launch / (gpu_ms_per_step * 1e-3) / 1e9
-    traffic = None if cfg5 else load_traffic(n, args.stack)
+    traffic = None if cfg5 else load_traffic(n, args.stack, envs.state_bytes_per_env)
     out = {
         "metric": METRIC,
         "value": round(value, 1),

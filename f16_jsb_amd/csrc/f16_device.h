@@ -85,36 +85,25 @@ static constexpr float RAD2DEG_F = 57.295779513082320876798f;
 // ------------------------------------------------------------------------------------------
 // lane state (registers) and its struct-of-arrays image in HBM
 // ------------------------------------------------------------------------------------------
-enum DField { D_RI0, D_RI1, D_RI2, D_VI0, D_VI1, D_VI2, D_EPA, D_EPRET, NDF };
-enum FField {
-  F_DV1 = 0,   // AB3 history as deltas: vI(k-1) - vI(k), vI(k-2) - vI(k)   (3+3)
-  F_DV2 = 3,
-  F_AI = 6,    // latest / previous inertial acceleration                   (3+3)
-  F_AIP = 9,
-  F_Q = 12,    // quaternion ECI->body                                      (4)
-  F_WI = 16,   // body rates wrt ECI                                        (3)
-  F_WID = 19,  // PQRidot                                                   (3)
-  F_BA = 22,   // body specific-force acceleration                          (3)
-  F_TEF = 25, F_AIL, F_ELE, F_RUD, F_LEF, F_SB,
-  F_PRI, F_PRP, F_PPI, F_PPP, F_PYI, F_PYP,
-  F_N1, F_N2,
-  F_LX,        // 10-entry auxiliary latch (F16L_*)
-  F_GOAL = F_LX + F16L_N,
-  F_LASTD = F_GOAL + 3,
-  F_WIND,
-  F_GUST = F_WIND + 3,  // cfg5 gust (NED fps); loaded/stored only by the gust-mode kernels
-  NFF = F_GUST + 3
-};
-enum IField { I_STEP, I_EPCOUNT, I_FLAGS, NIF };
+// Layout: 16-byte columns, column j of env k at c[j * n + k] (float4). A wave moves each
+// column with one coalesced dwordx4 access (1 KiB per wave-instruction): 19 wide loads and
+// stores per lane instead of 67 dword ones -- the step's store tail is issue-bound at 4 B/lane
+// (MI355X_MICROARCH.md, epilogue store tail). fp64 fields occupy two lanes of a column.
+//   C0  rI.x rI.y (f64)        C7  q0 q1 q2 q3            C14 lx1 lx2 lx3 lx4
+//   C1  rI.z vI.x (f64)        C8  wI.xyz wId.x           C15 lx5 lx6 lx7 lx8
+//   C2  vI.y vI.z (f64)        C9  wId.yz ba.xy           C16 lx9 goal.xyz
+//   C3  epa ep_ret (f64)       C10 ba.z tef ail ele       C17 last_d wind.xyz (steady)
+//   C4  dv1.xyz dv2.x          C11 rud lef sb pid_r_i     C18 step ep_count flags (i32), 0
+//   C5  dv2.yz aI.xy           C12 pid_r_p pid_p_i pid_p_p pid_y_i
+//   C6  aI.z aIp.xyz           C13 pid_y_p n1 n2 lx0      C19 gust.xyz, 0 (cfg5 gust mode only)
+enum { NCOL = 19, NCOL_ALL = 20, COL_GUST = 19 };
 static constexpr int LANE_FLAG_AUG = 1;
-// persistent bytes per env (SURVEY.md 8d "S"); the gust columns move only in gust mode
-static constexpr int STATE_BYTES = NDF * 8 + (NFF - 3) * 4 + NIF * 4;
-static constexpr int STATE_BYTES_GUST = STATE_BYTES + 12;
+// persistent bytes per env moved by a step (SURVEY.md 8d "S"); +16 in gust mode
+static constexpr int STATE_BYTES = NCOL * 16;
+static constexpr int STATE_BYTES_GUST = NCOL_ALL * 16;
 
 struct SoA {
-  double* d;
-  float* f;
-  int32_t* i;
+  float4* c;  // NCOL_ALL columns of n float4
   int64_t n;
 };
 
@@ -127,94 +116,76 @@ struct Lane {
   float lx[F16L_N];
   float goal[3], last_d;
   float wind[3];  // wind the FDM sees (NED fps): steady + gust
-  float wst[3];   // steady wind (SoA F_WIND); the gust-mode kernels keep it apart from
-  float gust[3];  // the cfg5 gust (SoA F_GUST)
+  float wst[3];   // steady wind (column 17); the gust-mode kernels keep it apart from
+  float gust[3];  // the cfg5 gust (column 19)
   int32_t step, ep_count, flags;
 };
+
+__device__ __forceinline__ double f2d(float lo, float hi) {
+  return __hiloint2double(__float_as_int(hi), __float_as_int(lo));
+}
+__device__ __forceinline__ float dlo(double d) { return __int_as_float(__double2loint(d)); }
+__device__ __forceinline__ float dhi(double d) { return __int_as_float(__double2hiint(d)); }
 
 template <bool GUST = false>
 __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   const int64_t n = s.n;
-
+  float4 c[NCOL];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    L.rI[j] = s.d[(D_RI0 + j) * n + k];
-    L.vI[j] = s.d[(D_VI0 + j) * n + k];
-  }
-  L.epa = s.d[D_EPA * n + k];
-  L.ep_ret = s.d[D_EPRET * n + k];
-  float* fl = reinterpret_cast<float*>(&L.dv1[0]);
-  (void)fl;
+  for (int j = 0; j < NCOL; ++j) c[j] = s.c[j * n + k];
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (GUST) g = s.c[COL_GUST * n + k];
+  L.rI[0] = f2d(c[0].x, c[0].y); L.rI[1] = f2d(c[0].z, c[0].w);
+  L.rI[2] = f2d(c[1].x, c[1].y); L.vI[0] = f2d(c[1].z, c[1].w);
+  L.vI[1] = f2d(c[2].x, c[2].y); L.vI[2] = f2d(c[2].z, c[2].w);
+  L.epa = f2d(c[3].x, c[3].y); L.ep_ret = f2d(c[3].z, c[3].w);
+  L.dv1[0] = c[4].x; L.dv1[1] = c[4].y; L.dv1[2] = c[4].z; L.dv2[0] = c[4].w;
+  L.dv2[1] = c[5].x; L.dv2[2] = c[5].y; L.aI[0] = c[5].z; L.aI[1] = c[5].w;
+  L.aI[2] = c[6].x; L.aIp[0] = c[6].y; L.aIp[1] = c[6].z; L.aIp[2] = c[6].w;
+  L.q[0] = c[7].x; L.q[1] = c[7].y; L.q[2] = c[7].z; L.q[3] = c[7].w;
+  L.wI[0] = c[8].x; L.wI[1] = c[8].y; L.wI[2] = c[8].z; L.wId[0] = c[8].w;
+  L.wId[1] = c[9].x; L.wId[2] = c[9].y; L.ba[0] = c[9].z; L.ba[1] = c[9].w;
+  L.ba[2] = c[10].x; L.tef = c[10].y; L.ail = c[10].z; L.ele = c[10].w;
+  L.rud = c[11].x; L.lef = c[11].y; L.sb = c[11].z; L.pri = c[11].w;
+  L.prp = c[12].x; L.ppi = c[12].y; L.ppp = c[12].z; L.pyi = c[12].w;
+  L.pyp = c[13].x; L.n1 = c[13].y; L.n2 = c[13].z; L.lx[0] = c[13].w;
+  L.lx[1] = c[14].x; L.lx[2] = c[14].y; L.lx[3] = c[14].z; L.lx[4] = c[14].w;
+  L.lx[5] = c[15].x; L.lx[6] = c[15].y; L.lx[7] = c[15].z; L.lx[8] = c[15].w;
+  L.lx[9] = c[16].x; L.goal[0] = c[16].y; L.goal[1] = c[16].z; L.goal[2] = c[16].w;
+  L.last_d = c[17].x; L.wst[0] = c[17].y; L.wst[1] = c[17].z; L.wst[2] = c[17].w;
+  L.step = __float_as_int(c[18].x); L.ep_count = __float_as_int(c[18].y); L.flags = __float_as_int(c[18].z);
+  L.gust[0] = g.x; L.gust[1] = g.y; L.gust[2] = g.z;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    L.dv1[j] = s.f[(F_DV1 + j) * n + k];
-    L.dv2[j] = s.f[(F_DV2 + j) * n + k];
-    L.aI[j] = s.f[(F_AI + j) * n + k];
-    L.aIp[j] = s.f[(F_AIP + j) * n + k];
-    L.wI[j] = s.f[(F_WI + j) * n + k];
-    L.wId[j] = s.f[(F_WID + j) * n + k];
-    L.ba[j] = s.f[(F_BA + j) * n + k];
-    L.goal[j] = s.f[(F_GOAL + j) * n + k];
-    L.wst[j] = s.f[(F_WIND + j) * n + k];
-    L.gust[j] = GUST ? s.f[(F_GUST + j) * n + k] : 0.0f;
-    L.wind[j] = GUST ? L.wst[j] + L.gust[j] : L.wst[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) L.q[j] = s.f[(F_Q + j) * n + k];
-  L.tef = s.f[F_TEF * n + k]; L.ail = s.f[F_AIL * n + k]; L.ele = s.f[F_ELE * n + k];
-  L.rud = s.f[F_RUD * n + k]; L.lef = s.f[F_LEF * n + k]; L.sb = s.f[F_SB * n + k];
-  L.pri = s.f[F_PRI * n + k]; L.prp = s.f[F_PRP * n + k];
-  L.ppi = s.f[F_PPI * n + k]; L.ppp = s.f[F_PPP * n + k];
-  L.pyi = s.f[F_PYI * n + k]; L.pyp = s.f[F_PYP * n + k];
-  L.n1 = s.f[F_N1 * n + k]; L.n2 = s.f[F_N2 * n + k];
-#pragma unroll
-  for (int j = 0; j < F16L_N; ++j) L.lx[j] = s.f[(F_LX + j) * n + k];
-  L.last_d = s.f[F_LASTD * n + k];
-  L.step = s.i[I_STEP * n + k];
-  L.ep_count = s.i[I_EPCOUNT * n + k];
-  L.flags = s.i[I_FLAGS * n + k];
+  for (int j = 0; j < 3; ++j) L.wind[j] = GUST ? L.wst[j] + L.gust[j] : L.wst[j];
 }
 
 template <bool GUST = false>
 __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
   const int64_t n = s.n;
-  if (GUST) {
+  float4 c[NCOL];
+  c[0] = make_float4(dlo(L.rI[0]), dhi(L.rI[0]), dlo(L.rI[1]), dhi(L.rI[1]));
+  c[1] = make_float4(dlo(L.rI[2]), dhi(L.rI[2]), dlo(L.vI[0]), dhi(L.vI[0]));
+  c[2] = make_float4(dlo(L.vI[1]), dhi(L.vI[1]), dlo(L.vI[2]), dhi(L.vI[2]));
+  c[3] = make_float4(dlo(L.epa), dhi(L.epa), dlo(L.ep_ret), dhi(L.ep_ret));
+  c[4] = make_float4(L.dv1[0], L.dv1[1], L.dv1[2], L.dv2[0]);
+  c[5] = make_float4(L.dv2[1], L.dv2[2], L.aI[0], L.aI[1]);
+  c[6] = make_float4(L.aI[2], L.aIp[0], L.aIp[1], L.aIp[2]);
+  c[7] = make_float4(L.q[0], L.q[1], L.q[2], L.q[3]);
+  c[8] = make_float4(L.wI[0], L.wI[1], L.wI[2], L.wId[0]);
+  c[9] = make_float4(L.wId[1], L.wId[2], L.ba[0], L.ba[1]);
+  c[10] = make_float4(L.ba[2], L.tef, L.ail, L.ele);
+  c[11] = make_float4(L.rud, L.lef, L.sb, L.pri);
+  c[12] = make_float4(L.prp, L.ppi, L.ppp, L.pyi);
+  c[13] = make_float4(L.pyp, L.n1, L.n2, L.lx[0]);
+  c[14] = make_float4(L.lx[1], L.lx[2], L.lx[3], L.lx[4]);
+  c[15] = make_float4(L.lx[5], L.lx[6], L.lx[7], L.lx[8]);
+  c[16] = make_float4(L.lx[9], L.goal[0], L.goal[1], L.goal[2]);
+  c[17] = GUST ? make_float4(L.last_d, L.wst[0], L.wst[1], L.wst[2])
+               : make_float4(L.last_d, L.wind[0], L.wind[1], L.wind[2]);
+  c[18] = make_float4(__int_as_float(L.step), __int_as_float(L.ep_count), __int_as_float(L.flags), 0.0f);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) s.f[(F_GUST + j) * n + k] = L.gust[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    s.d[(D_RI0 + j) * n + k] = L.rI[j];
-    s.d[(D_VI0 + j) * n + k] = L.vI[j];
-  }
-  s.d[D_EPA * n + k] = L.epa;
-  s.d[D_EPRET * n + k] = L.ep_ret;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    s.f[(F_DV1 + j) * n + k] = L.dv1[j];
-    s.f[(F_DV2 + j) * n + k] = L.dv2[j];
-    s.f[(F_AI + j) * n + k] = L.aI[j];
-    s.f[(F_AIP + j) * n + k] = L.aIp[j];
-    s.f[(F_WI + j) * n + k] = L.wI[j];
-    s.f[(F_WID + j) * n + k] = L.wId[j];
-    s.f[(F_BA + j) * n + k] = L.ba[j];
-    s.f[(F_GOAL + j) * n + k] = L.goal[j];
-    s.f[(F_WIND + j) * n + k] = GUST ? L.wst[j] : L.wind[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s.f[(F_Q + j) * n + k] = L.q[j];
-  s.f[F_TEF * n + k] = L.tef; s.f[F_AIL * n + k] = L.ail; s.f[F_ELE * n + k] = L.ele;
-  s.f[F_RUD * n + k] = L.rud; s.f[F_LEF * n + k] = L.lef; s.f[F_SB * n + k] = L.sb;
-  s.f[F_PRI * n + k] = L.pri; s.f[F_PRP * n + k] = L.prp;
-  s.f[F_PPI * n + k] = L.ppi; s.f[F_PPP * n + k] = L.ppp;
-  s.f[F_PYI * n + k] = L.pyi; s.f[F_PYP * n + k] = L.pyp;
-  s.f[F_N1 * n + k] = L.n1; s.f[F_N2 * n + k] = L.n2;
-#pragma unroll
-  for (int j = 0; j < F16L_N; ++j) s.f[(F_LX + j) * n + k] = L.lx[j];
-  s.f[F_LASTD * n + k] = L.last_d;
-  s.i[I_STEP * n + k] = L.step;
-  s.i[I_EPCOUNT * n + k] = L.ep_count;
-  s.i[I_FLAGS * n + k] = L.flags;
+  for (int j = 0; j < NCOL; ++j) s.c[j * n + k] = c[j];
+  if (GUST) s.c[COL_GUST * n + k] = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -866,15 +866,10 @@ struct f16env {
 };
 
 static void soa_carve(void* base, int64_t n, SoA& s) {
-  char* p = (char*)base;
   s.n = n;
-  s.d = (double*)p;
-  p += sizeof(double) * NDF * n;
-  s.f = (float*)p;
-  p += sizeof(float) * NFF * n;
-  s.i = (int32_t*)p;
+  s.c = (float4*)base;
 }
-static size_t soa_bytes(int64_t n) { return (size_t)n * (NDF * 8 + NFF * 4 + NIF * 4); }
+static size_t soa_bytes(int64_t n) { return (size_t)n * NCOL_ALL * 16; }
 
 // Same mass-balance / constants derivation as oracle init_consts() (f16.xml:37-83,245-300).
 static void build_consts(const f16env_config& cfg, ModelConsts& C) {

@@ -43,9 +43,10 @@ def main():
     write_kib, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel, a.envs)
     rd = 2.0 * fetch_kib * 1024.0
     wr = write_kib * 1024.0
-    alg = algorithmic_bytes_per_env_step(a.stack, int(lib().f16env_state_bytes_per_env())) * a.envs
+    state_bytes = int(lib().f16env_state_bytes_per_env())
+    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes) * a.envs
     d = {
-        "kernel": a.kernel, "envs": a.envs, "stack_k": a.stack,
+        "kernel": a.kernel, "envs": a.envs, "stack_k": a.stack, "state_bytes": state_bytes,
         "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib, "launches": [nf, nw],
         "hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
         "hbm_bytes_per_launch": int(rd + wr),
