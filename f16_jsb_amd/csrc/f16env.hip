@@ -290,8 +290,30 @@ __device__ __forceinline__ void lane_reset_template(Lane& L, const SoA& tmpl, co
 #endif
 #define FRAME_PITCH 16
 
+// LDS-DMA of 16 B per lane: lane i's 16 bytes land at lds + 16*i (gfx950 global_load_lds_dwordx4)
+__device__ __forceinline__ void dma16(const float* g, float* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
+}
+// ... and of 4 B per lane (lane i's dword lands at lds + 4*i)
+__device__ __forceinline__ void dma4(const float* g, float* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)lds, 4, 0, 0);
+}
+// Table blob -> LDS by LDS-DMA (no VGPRs, no wait at issue): the caller issues its other
+// loads behind it and completes the staging with one s_waitcnt vmcnt(0) + barrier.
+__device__ __forceinline__ void stage_tables_issue(float* sT) {
+  constexpr int NP = F16_BLOB_FLOATS / 4;  // 16-byte pieces (the generator pads the blob)
+  static_assert(F16_BLOB_FLOATS % 4 == 0, "blob must be whole 16-byte pieces");
+  const int wave_base = threadIdx.x & ~63;
+  for (int r = 0; r < NP; r += blockDim.x) {
+    const int piece = r + threadIdx.x;
+    if (piece < NP) dma16(F16_BLOB_INIT + 4 * piece, sT + 4 * (r + wave_base));
+  }
+}
 __device__ __forceinline__ void stage_tables(float* sT) {
-  for (int j = threadIdx.x; j < F16_BLOB_FLOATS; j += blockDim.x) sT[j] = F16_BLOB_INIT[j];
+  stage_tables_issue(sT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 }
 
@@ -317,11 +339,6 @@ struct StepArgs {
 __device__ unsigned long long g_stamps[1 << 14][ST_N];  // per wave (diagnostic build)
 #endif
 
-// LDS-DMA of 16 B per lane: lane i's 16 bytes land at lds + 16*i (gfx950 global_load_lds_dwordx4)
-__device__ __forceinline__ void dma16(const float* g, float* lds) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
-                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
-}
 
 // Dynamic LDS: image mode holds, per wave, the previous stack block of its 64 rows
 // (64*KC floats) + one spare frame; fallback mode holds the final/reset frames per lane.
@@ -353,10 +370,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
         const int piece = b + lane;
         if (piece < n16) dma16(prev + 4 * piece, img + 4 * b);
       }
-      if (lane < (total & 3)) img[4 * n16 + lane] = prev[4 * n16 + lane];  // tail, never past the end
+      if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + 4 * n16);  // tail, never past the end
     }
   };
-#ifndef F16_DMA_LATE
+#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA)
   issue_stack_dma();
 #endif
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -364,17 +381,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
   int done = 0;
   Lane L;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (live) {  // issue the state loads before the table staging so their latencies overlap
+  // every load of the prologue is in flight at once (stack DMA above, table DMA, state and
+  // action loads), then one wait: a single HBM round trip before the physics
+  stage_tables_issue(sT);
+  if (live) {
     lane_load<GUST>(a.s, k, L);
     av = reinterpret_cast<const float4*>(a.act)[k];
   }
-  stage_tables(sT);
-#ifdef F16_DMA_LATE
-  // the state loads first get the full HBM bandwidth; the stack DMA then streams under the
-  // physics (it is only needed at the splice)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  issue_stack_dma();
-#endif
+  __syncthreads();
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   if (live) {
@@ -438,7 +453,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
       }
     }
     F16_STAMP(stamps, ST_RESET);
+#ifndef F16_DIAG_SKIP_STORE
     lane_store<GUST>(a.s, k, L);
+#else
+    if (L.step == -12345) lane_store<GUST>(a.s, k, L);
+#endif
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
@@ -454,17 +473,25 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
   }
   // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel
   const bool autoreset = !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET);
-  if (image) {
+  // F16_DIAG_SKIP_* : timing experiments only (results are wrong with them)
+#ifdef F16_DIAG_SKIP_STACK
+  constexpr bool kSkipStack = true;
+#else
+  constexpr bool kSkipStack = false;
+#endif
+  if (kSkipStack) {
+  } else if (image) {
     // 2) splice the new frame of row r into the image at row r+1's first frame, which the
-    //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block. The stack
+    //    DMA landed at the prologue wait, and a wave only touches its own image, so the steps
+    //    below need no workgroup barrier (a wave's LDS accesses complete in order).
+    __builtin_amdgcn_wave_barrier();
     if (live) {
       float* dst = img + (size_t)(lane + 1) * KC;
 #pragma unroll
       for (int j = 0; j < F16_OBS_DIM; ++j) dst[j] = f[j];
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     // 3) finished rows: terminal obs = the spliced row; then the row becomes K x frame 0
     if (live && done) {
       float* src = img + (size_t)lane * KC + F16_OBS_DIM;
@@ -475,17 +502,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
       if (autoreset)
         for (int c = 0; c < KC; ++c) src[c] = f0[c % F16_OBS_DIM];
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     F16_STAMP(stamps, ST_SYNC);
     // 4) one coalesced float4 copy of the block (obs blocks are 16-B aligned per wave)
     if (rows > 0) {
       float* out = a.obs + row0 * KC;
       const int total = rows * KC, n4 = total >> 2;
       float4* out4 = reinterpret_cast<float4*>(out);
+#ifndef F16_DIAG_SKIP_COPYOUT
       for (int q = lane; q < n4; q += 64) {
         const float* p = img + 4 * q + F16_OBS_DIM;
         out4[q] = make_float4(p[0], p[1], p[2], p[3]);
       }
+#endif
       for (int j = 4 * n4 + lane; j < total; j += 64) out[j] = img[j + F16_OBS_DIM];
     }
     F16_STAMP(stamps, ST_COPY);

@@ -364,7 +364,7 @@ def emit_kernel(model, path):
                 eng_u.append(t["data"][ii][j])
     put("engu_v", eng_u)
     # (lo, 1/span) pairs for LDS brackets (8-byte aligned for ds_read_b64)
-    if len(blob) % 2:
+    while len(blob) % 4:  # whole 16-byte pieces: the kernels stage the blob by LDS-DMA
         blob.append(0.0)
 
     def pairs(bp):
@@ -377,7 +377,7 @@ def emit_kernel(model, path):
         put("pair_" + key, pairs(bp))
     for n, t in model["fcs_tables"].items():
         put("pair_fcs_" + n.split("/")[-1], pairs(t["rows"]))
-    if len(blob) % 2:
+    while len(blob) % 4:  # whole 16-byte pieces: the kernels stage the blob by LDS-DMA
         blob.append(0.0)
 
     L = ["/* GENERATED by tools/gen_tables.py from the reference's f16.xml / F100-PW-229.xml.",
@@ -430,7 +430,7 @@ def emit_kernel(model, path):
         L.append("static constexpr float BP_engr_%s[%d] = {%s};" % (n, nr, ", ".join(_lit(v, "%.9gf") for v in t["rows"])))
         L.append("static constexpr float BP_engc_%s[%d] = {%s};" % (n, nc, ", ".join(_lit(v, "%.9gf") for v in t["cols"])))
     L.append("")
-    L.append("__device__ const float F16_BLOB_INIT[F16_BLOB_FLOATS] = {")
+    L.append("__device__ __attribute__((aligned(16))) const float F16_BLOB_INIT[F16_BLOB_FLOATS] = {")
     L.append(_fmt(blob, per=8, fmt="%.9gf"))
     L.append("};")
     with open(path, "w") as fh:

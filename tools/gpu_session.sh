@@ -46,6 +46,8 @@ for s in $STEPS; do
       run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_sq_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- \
+        python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
+      run pmc_sq3 600 rocprofv3 --pmc SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 -d "$OUT/pmc_sq3_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0 ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- \
