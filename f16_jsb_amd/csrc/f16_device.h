@@ -127,14 +127,8 @@ __device__ __forceinline__ double f2d(float lo, float hi) {
 __device__ __forceinline__ float dlo(double d) { return __int_as_float(__double2loint(d)); }
 __device__ __forceinline__ float dhi(double d) { return __int_as_float(__double2hiint(d)); }
 
-template <bool GUST = false>
-__device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
-  const int64_t n = s.n;
-  float4 c[NCOL];
-#pragma unroll
-  for (int j = 0; j < NCOL; ++j) c[j] = s.c[j * n + k];
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (GUST) g = s.c[COL_GUST * n + k];
+template <bool GUST>
+__device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 g, Lane& L) {
   L.rI[0] = f2d(c[0].x, c[0].y); L.rI[1] = f2d(c[0].z, c[0].w);
   L.rI[2] = f2d(c[1].x, c[1].y); L.vI[0] = f2d(c[1].z, c[1].w);
   L.vI[1] = f2d(c[2].x, c[2].y); L.vI[2] = f2d(c[2].z, c[2].w);
@@ -157,6 +151,24 @@ __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   L.gust[0] = g.x; L.gust[1] = g.y; L.gust[2] = g.z;
 #pragma unroll
   for (int j = 0; j < 3; ++j) L.wind[j] = GUST ? L.wst[j] + L.gust[j] : L.wst[j];
+}
+template <bool GUST = false>
+__device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
+  const int64_t n = s.n;
+  float4 c[NCOL];
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) c[j] = s.c[j * n + k];
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (GUST) g = s.c[COL_GUST * n + k];
+  lane_unpack<GUST>(c, g, L);
+}
+// the one-env IC template staged in LDS (columns contiguous): no vector-memory traffic, so
+// the reset of a finished lane adds no vmcnt dependency to the step's store tail
+__device__ __forceinline__ void lane_load_lds(const float4* cols, Lane& L) {
+  float4 c[NCOL];
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) c[j] = cols[j];
+  lane_unpack<false>(c, make_float4(0.f, 0.f, 0.f, 0.f), L);
 }
 
 template <bool GUST = false>

@@ -270,10 +270,10 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
 }
 
-__device__ __forceinline__ void lane_reset_template(Lane& L, const SoA& tmpl, const EnvArgs& E, int64_t k,
+__device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl, const EnvArgs& E, int64_t k,
                                                     float* f0) {
   const int32_t ep = L.ep_count;
-  lane_load(tmpl, 0, L);
+  lane_load_lds(sTmpl, L);
   rng_goal(E.seed, (uint64_t)(E.id_base + k), (uint32_t)ep, L.goal);
   L.ep_count = ep + 1;
   L.step = 0;
@@ -348,7 +348,7 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // finished lanes inline from the IC template; other modes leave finished lanes to
 // f16_reset_done_kernel (a full RunIC per lane is too long to run divergently in-wave).
 template <int MODE>
-__device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDone, float* dynl) {
+__device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* sTmpl, int* sDone, float* dynl) {
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
 #ifdef F16_STAMPS
   Stamps stamps = {};
@@ -384,6 +384,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
   // every load of the prologue is in flight at once (stack DMA above, table DMA, state and
   // action loads), then one wait: a single HBM round trip before the physics
   stage_tables_issue(sT);
+  if (!DEFER && threadIdx.x < NCOL) dma16(reinterpret_cast<const float*>(a.tmpl.c + threadIdx.x),
+                                          reinterpret_cast<float*>(sTmpl));
   if (live) {
     lane_load<GUST>(a.s, k, L);
     av = reinterpret_cast<const float4*>(a.act)[k];
@@ -392,6 +394,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
   __syncthreads();
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
+  float rew_out = 0.0f;
+  int flags_out = 0;
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
@@ -438,15 +442,30 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
       r32 = (float)r;
     }
     F16_STAMP(stamps, ST_REWARD);
-    a.rew[k] = r32;
-    a.term[k] = (uint8_t)te;
-    a.trunc[k] = (uint8_t)tr;
     done = te | tr;
+    rew_out = r32;
+    flags_out = te | (tr << 1);
+  }
+  // compaction of finished lanes (wave64 ballot), before any store of this step so the
+  // atomic's return waits on nothing else
+  if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)
+    const unsigned long long m = __ballot(done);
+    if (m) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(a.n_done, __popcll(m));
+      base = __shfl(base, 0);
+      if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
+    }
+  }
+  if (live) {
+    a.rew[k] = rew_out;
+    a.term[k] = (uint8_t)(flags_out & 1);
+    a.trunc[k] = (uint8_t)(flags_out >> 1);
     if (done) {
       if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
       if (a.ep_len) a.ep_len[k] = L.step;
       if (!DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)) {
-        lane_reset_template(L, a.tmpl, a.E, k, f0);
+        lane_reset_template(L, sTmpl, a.E, k, f0);
       } else {
 #pragma unroll
         for (int j = 0; j < F16_OBS_DIM; ++j) f0[j] = f[j];
@@ -461,16 +480,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
-  // compaction of finished lanes (wave64 ballot)
-  if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)
-    const unsigned long long m = __ballot(done);
-    int base = 0;
-    if (m) {
-      if (lane == 0) base = atomicAdd(a.n_done, __popcll(m));
-      base = __shfl(base, 0);
-      if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
-    }
-  }
   // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel
   const bool autoreset = !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET);
   // F16_DIAG_SKIP_* : timing experiments only (results are wrong with them)
@@ -586,6 +595,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
 
 #define STEP_SHARED                                       \
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];   \
+  __shared__ __align__(16) float4 sTmpl[NCOL];            \
   __shared__ int sDone[BLOCK];                            \
   extern __shared__ __align__(16) float dynl[];
 
@@ -595,12 +605,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, int* sDo
 // memory phases and stalls with the other's VALU work (f16env_step picks per launch).
 __global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(StepArgs a) {
   STEP_SHARED
-  step_body<0>(a, sT, sDone, dynl);
+  step_body<0>(a, sT, sTmpl, sDone, dynl);
 }
 template <int MODE, int OCC>
 __global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
   STEP_SHARED
-  step_body<MODE>(a, sT, sDone, dynl);
+  step_body<MODE>(a, sT, sTmpl, sDone, dynl);
 }
 using StepKernel = void (*)(StepArgs);
 static StepKernel step_kernel_for(int mode, int occ) {
@@ -1048,7 +1058,7 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const int KC = cfg->stack_k * F16_OBS_DIM;
     const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
     const size_t fallback = sizeof(float) * 2 * BLOCK * FRAME_PITCH;
-    const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + sizeof(int) * BLOCK + 64;
+    const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + 16 * NCOL + sizeof(int) * BLOCK + 64;
     h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : 0;
     h->dyn_lds = h->lds_image ? img : fallback;
     for (int occ = 1; occ <= 2; ++occ)
