@@ -292,14 +292,13 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   for (int k = 1; k < 7; ++k) {
     if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; ex = EX[k]; }
   }
-  float T, P;
-  if (lb != 0.0f) {
-    T = tb + lb * (H - hb);
-    P = pb * __powf(tb * rcpf(T), ex);
-  } else {
-    T = tb;
-    P = pb * __expf(-GMR * (H - hb) * rcpf(tb));
-  }
+  // P = pb (tb/T)^ex in the gradient layers, pb exp(-GMR (H - hb) / tb) in the isothermal
+  // ones: both as one v_log_f32 + one v_exp_f32, branch-free (OCML powf is ~130 VALU of
+  // compensated double-float arithmetic; v_log/v_exp keep P within ~1e-7 relative)
+  const float T = tb + lb * (H - hb);
+  const float lg2 = (lb != 0.0f) ? ex * __builtin_amdgcn_logf(tb * rcpf(T))
+                                 : (-GMR * 1.4426950408889634f) * (H - hb) * rcpf(tb);
+  const float P = pb * __builtin_amdgcn_exp2f(lg2);
   const float rho = P * rcpf(R * T);
   Atm o;
   o.T = T * 1.8f;
@@ -322,7 +321,7 @@ __device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts
   }
   const float qc = pt - p;
   const float A = qc * C.inv_p_sl + 1.0f;
-  float M = fsqrt(5.0f * (__powf(A, 1.0f / 3.5f) - 1.0f));
+  float M = fsqrt(5.0f * (__builtin_amdgcn_exp2f((1.0f / 3.5f) * __builtin_amdgcn_logf(A)) - 1.0f));
   if (M > 1.0f) {
     for (int i = 0; i < 10; ++i) {
       float t = 1.0f - rcpf(7.0f * M * M);
@@ -806,7 +805,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     float n1 = q0 * p1 + q1 * p0 + q2 * p3 - q3 * p2;
     float n2 = q0 * p2 - q1 * p3 + q2 * p0 + q3 * p1;
     float n3 = q0 * p3 + q1 * p2 - q2 * p1 + q3 * p0;
-    const float rn = rsqrtf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+    const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);  // |n| ~ 1
     L.q[0] = n0 * rn; L.q[1] = n1 * rn; L.q[2] = n2 * rn; L.q[3] = n3 * rn;
 #pragma unroll
     for (int j = 0; j < 3; ++j) L.wI[j] += dt * L.wId[j];

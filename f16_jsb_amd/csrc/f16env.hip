@@ -373,7 +373,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
       if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + 4 * n16);  // tail, never past the end
     }
   };
-#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA)
+#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && defined(F16_DMA_FIRST)
   issue_stack_dma();
 #endif
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -381,8 +381,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
   int done = 0;
   Lane L;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
-  // every load of the prologue is in flight at once (stack DMA above, table DMA, state and
-  // action loads), then one wait: a single HBM round trip before the physics
+  // the loads the physics needs are in flight at once (table DMA, IC template, state and
+  // action), then one wait: a single HBM round trip before the physics. The previous stack
+  // (only needed by the obs rebuild) is DMA'd after that wait, so it streams in while the
+  // first frame runs instead of sharing the prologue's HBM bandwidth.
   stage_tables_issue(sT);
   if (!DEFER && threadIdx.x < NCOL) dma16(reinterpret_cast<const float*>(a.tmpl.c + threadIdx.x),
                                           reinterpret_cast<float*>(sTmpl));
@@ -392,6 +394,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && !defined(F16_DMA_FIRST)
+  issue_stack_dma();
+#endif
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   float rew_out = 0.0f;
@@ -446,6 +451,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
     rew_out = r32;
     flags_out = te | (tr << 1);
   }
+  // the stack DMA issued after the prologue has long landed; retire it here, before any
+  // store of this step (vmcnt also counts stores on CDNA, so a later wait would drain them)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // compaction of finished lanes (wave64 ballot), before any store of this step so the
   // atomic's return waits on nothing else
   if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)

@@ -209,15 +209,17 @@ def test_trim_parity_and_level_flight(torch_mod):
     assert np.all(np.abs(o_r[:, -1, 2] - h0) < 60.0)
 
 
-def test_large_batch_properties(torch_mod):
+@pytest.mark.parametrize("n,k,steps", [(65536, 4, 200), (4171, 2, 40), (2113, 10, 40), (1000, 8, 40), (777, 3, 40)])
+def test_large_batch_properties(torch_mod, n, k, steps):
     """65 536 envs (BASELINE cfg3 shape), 200 random-action steps: finite outputs, the
     ordered-stack invariant obs[t][:, :-1] == obs[t-1][:, 1:] on continuing lanes
     (bit-exact), auto-reset rows are K copies, determinism across handles, and the
-    in-place (obs_prev == obs) ABI mode equals the ping-pong mode bit for bit."""
+    in-place (obs_prev == obs) ABI mode equals the ping-pong mode bit for bit. Smaller
+    ragged batches (partial last wave) and other stack depths cover the split early/late
+    obs rebuild and the flat-copy fallback."""
     torch = torch_mod
     from f16_jsb_amd.env import F16Envs
     from f16_jsb_amd._lib import lib
-    n, k = 65536, 4
     a = F16Envs(n, stack_k=k, seed=9)
     b = F16Envs(n, stack_k=k, seed=9)
     a.reset()
@@ -227,7 +229,7 @@ def test_large_batch_properties(torch_mod):
     L = lib()
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     n_done_total = 0
-    for t in range(200):
+    for t in range(steps):
         act = a.sample_actions(3, t)
         out = a.step(act)
         rc = L.f16env_step(b._h, stream, act.data_ptr(), inplace.data_ptr(), inplace.data_ptr(), b.rew.data_ptr(),
@@ -246,7 +248,7 @@ def test_large_batch_properties(torch_mod):
             r = out.obs[done]
             assert torch.equal(r, r[:, :1].expand_as(r))
         prev = out.obs.clone()
-    assert n_done_total > 0
+    assert n_done_total > 0 or n < 65536
 
 
 def test_done_index_compaction(torch_mod):
