@@ -258,11 +258,16 @@ __device__ __forceinline__ float fatan2(float y, float x) {
   return copysignf(r, y);
 }
 
-// 1-D lookup over LDS values with literal breakpoints and LDS (lo, 1/span) pairs
+// blend with a precomputed slope: v + f (v_next - v), the slope stored beside the value in
+// the blob (tools/gen_tables.py), i.e. the same fp32 FMA as lerp1 without the subtraction
+__device__ __forceinline__ float blend(float f, float v, float slope) { return __builtin_fmaf(f, slope, v); }
+
+// 1-D lookup: literal breakpoints, LDS (lo, 1/span) pairs, LDS (value, slope) pairs
 template <int N>
-__device__ __forceinline__ float tab1(const float (&bp)[N], const float* pairs, const float* v, float x) {
+__device__ __forceinline__ float tab1(const float (&bp)[N], const float* pairs, const float* vd, float x) {
   const Seg s = bracket(bp, pairs, x);
-  return lerp1(s.f, v[s.i - 1], v[s.i]);
+  const float2 p = reinterpret_cast<const float2*>(vd)[s.i - 1];
+  return blend(s.f, p.x, p.y);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -283,14 +288,18 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   constexpr float R = 8.31432f / 0.0289644f;
   const float z = h_ft * 0.3048f;
   const float H = 6356766.0f * z * rcpf(6356766.0f + z);
-  int b = 0;
-#pragma unroll
-  for (int k = 1; k < 7; ++k) b += (H >= Hb[k]) ? 1 : 0;
   constexpr float EX[7] = {GMR / Lb[0], 0.0f, GMR / Lb[2], GMR / Lb[3], 0.0f, GMR / Lb[5], GMR / Lb[6]};
   float hb = Hb[0], lb = Lb[0], tb = Tb[0], pb = Pb[0], ex = EX[0];
+  // layer search only when some lane of the wave is above the troposphere (wave-uniform
+  // branch; the reference task and the cfg5 IC box stay below 11 km almost always)
+  if (__builtin_expect(__ballot(H >= Hb[1]) != 0, 0)) {
+    int b = 0;
 #pragma unroll
-  for (int k = 1; k < 7; ++k) {
-    if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; ex = EX[k]; }
+    for (int k = 1; k < 7; ++k) b += (H >= Hb[k]) ? 1 : 0;
+#pragma unroll
+    for (int k = 1; k < 7; ++k) {
+      if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; ex = EX[k]; }
+    }
   }
   // P = pb (tb/T)^ex in the gradient layers, pb exp(-GMR (H - hb) / tb) in the isothermal
   // ones: both as one v_log_f32 + one v_exp_f32, branch-free (OCML powf is ~130 VALU of
@@ -323,10 +332,22 @@ __device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts
   const float A = qc * C.inv_p_sl + 1.0f;
   float M = fsqrt(5.0f * (__builtin_amdgcn_exp2f((1.0f / 3.5f) * __builtin_amdgcn_logf(A)) - 1.0f));
   if (M > 1.0f) {
-    for (int i = 0; i < 10; ++i) {
-      float t = 1.0f - rcpf(7.0f * M * M);
-      M = 0.8812848543473311f * fsqrt(A * (t * t * fsqrt(t)));
+    // Supersonic: the Rayleigh pitot relation M = c sqrt(A (1 - 1/(7 M^2))^2.5), which the
+    // oracle solves by 10 fixed-point steps (contraction ~0.3 per step, converged to fp32
+    // precision), solved here by Newton on y = M^2 from the subsonic estimate: 3 steps, each
+    // quadratically convergent (9 transcendentals instead of 30).
+    float y = M * M;
+    const float cA = 0.8812848543473311f * 0.8812848543473311f * A;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float iy = rcpf(y);
+      const float t = 1.0f - (1.0f / 7.0f) * iy;
+      const float tst = t * fsqrt(t);
+      const float g = cA * t * tst;                               // cA t^2.5
+      const float dg = (2.5f / 7.0f) * cA * tst * iy * iy;        // dg/dy
+      y -= (y - g) * rcpf(1.0f - dg);
     }
+    M = fsqrt(y);
   }
   return C.a_sl * M * C.kts_per_fps;
 }
@@ -534,6 +555,7 @@ __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic)
 #pragma unroll
   for (int g = 0; g < 3; ++g) {
     active = active && dt0 > 0.0f && !eq_roundoff(in, out);
+    if (__ballot(active) == 0) break;  // wave-uniform: the flaps are at their detent
     const bool down = in < out;
     const bool seg1 = down ? !(0.0f < out) : !(0.0f <= out);  // transition time 0 -> jump
     const float tin = clipf(in, 0.0f, 1.0f);
@@ -572,10 +594,10 @@ struct FcsTab {  // scheduled gains of the FCS, looked up from the previous fram
 __device__ __forceinline__ FcsTab fcs_tables(const Lane& L, const float* T) {
   FcsTab t;
   t.asc = tab1(BP_fcs_aileron_speed_compensated, T + OFF_pair_fcs_aileron_speed_compensated,
-               T + OFF_fcs_v_aileron_speed_compensated, L.lx[F16L_MACH]);
+               T + OFF_fcs_vd_aileron_speed_compensated, L.lx[F16L_MACH]);
   t.ele = tab1(BP_fcs_elevator_scheduler, T + OFF_pair_fcs_elevator_scheduler,
-               T + OFF_fcs_v_elevator_scheduler, L.lx[F16L_ALPHA]);
-  t.yaw = tab1(BP_fcs_yaw_rate_norm, T + OFF_pair_fcs_yaw_rate_norm, T + OFF_fcs_v_yaw_rate_norm,
+               T + OFF_fcs_vd_elevator_scheduler, L.lx[F16L_ALPHA]);
+  t.yaw = tab1(BP_fcs_yaw_rate_norm, T + OFF_pair_fcs_yaw_rate_norm, T + OFF_fcs_vd_yaw_rate_norm,
                L.lx[F16L_VG_FPS]);
   return t;
 }
@@ -628,7 +650,7 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   o.throttle = cmd[3] * 2.0f;
   // Speedbrake
   const float sb_init = (alpha * RAD2DEG_F >= 53.0f && v_fps <= 18.0f) ? 1.0f : 0.0f;
-  const float sb_sched = sb_init * T[OFF_fcs_v_speedbrake_scheduler];  // gear-cmd-norm = 0
+  const float sb_sched = sb_init * T[OFF_fcs_vd_speedbrake_scheduler];  // gear-cmd-norm = 0
   L.sb = kin2(L.sb, sb_sched * 60.0f, 0.0f, 60.0f, 60.0f, dt, ic);
   o.dsb = L.sb * (1.0f / RAD2DEG_F);
 }
@@ -644,17 +666,17 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   float tp = throttle_pos, aug_cmd = 0.0f;
   if (tp > 1.0f) { aug_cmd = tp - 1.0f; tp -= aug_cmd; }
   // IdleThrust / MilThrust / AugThrust on one (mach 0..2.6 step 0.2) x (density-alt
-  // -10000..60000 step 10000) grid, interleaved [14][8][3] (Idle/Mil rows clamped beyond
-  // their last mach row, as FGTable does)
+  // -10000..60000 step 10000) grid, [14][8][3 values | 3 mach-slopes] (Idle/Mil rows clamped
+  // beyond their last mach row, as FGTable does)
   const Seg er = bracket_uniform(mach, 0.0f, 5.0f, ENGU_NR);
   const Seg ec = bracket_uniform(h_rho, -10000.0f, 1e-4f, ENGU_NC);
-  const float* e00 = T + OFF_engu_v + ((er.i - 1) * ENGU_NC + ec.i - 1) * 3;
-  const float* e10 = e00 + ENGU_NC * 3;
+  const float* e00 = T + OFF_engu_v + ((er.i - 1) * ENGU_NC + ec.i - 1) * 6;
+  const float* e01 = e00 + 6;
   float ev[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float c1 = lerp1(er.f, e00[k], e10[k]);
-    const float c2 = lerp1(er.f, e00[k + 3], e10[k + 3]);
+    const float c1 = blend(er.f, e00[k], e00[k + 3]);
+    const float c2 = blend(er.f, e01[k], e01[k + 3]);
     ev[k] = c1 + ec.f * (c2 - c1);
   }
   const float idle = 17800.0f * ev[0];
@@ -690,59 +712,59 @@ struct AeroIn {
 };
 __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6) {
   const Seg sa = bracket(BP_alpha_bp, T + OFF_pair_alpha, a.alpha);
-  // 16 alpha 1-D tables, [12][16] interleaved; FGTable 1-D semantics (clamp at the ends)
+  // 16 alpha 1-D tables, [12][16 values | 16 alpha-slopes]; FGTable 1-D semantics (clamp
+  // at the ends)
   float A[F16_N_A1D];
   {
-    const float* r0 = T + OFF_alpha1d + (sa.i - 1) * F16_N_A1D;
-    const float* r1 = r0 + F16_N_A1D;
+    const float* r0 = T + OFF_alpha1d + (sa.i - 1) * (2 * F16_N_A1D);
 #pragma unroll
-    for (int k = 0; k < F16_N_A1D; ++k) A[k] = lerp1(sa.f, r0[k], r1[k]);
+    for (int k = 0; k < F16_N_A1D; ++k) A[k] = blend(sa.f, r0[k], r0[F16_N_A1D + k]);
   }
-  // 2-D alpha x elevator: CDDh, CLDh, CmDh ([12][5][3])
+  // 2-D over (alpha, X), entries [12][X][G values | G alpha-slopes]: blend along alpha at the
+  // two bracketing X columns, then along X
   const Seg se = bracket(BP_de_bp, T + OFF_pair_de, a.de);
-  float ADE[3];
+  float ADE[3];  // CDDh, CLDh, CmDh over (alpha, elevator)
   {
-    const float* p00 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 3;
-    const float* p10 = p00 + F16_N_DE * 3;
+    const float* p0 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 6;
+    const float* p1 = p0 + 6;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const float c1 = lerp1(sa.f, p00[k], p10[k]);
-      const float c2 = lerp1(sa.f, p00[k + 3], p10[k + 3]);
+      const float c1 = blend(sa.f, p0[k], p0[k + 3]);
+      const float c2 = blend(sa.f, p1[k], p1[k + 3]);
       ADE[k] = c1 + se.f * (c2 - c1);
     }
   }
   const Seg sb13 = bracket(BP_beta13_bp, T + OFF_pair_beta13, a.beta);
-  float AB13[2];
+  float AB13[2];  // Clb, Cnb over (alpha, beta 13)
   {
-    const float* p00 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 2;
-    const float* p10 = p00 + F16_N_B13 * 2;
+    const float* p0 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 4;
+    const float* p1 = p0 + 4;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const float c1 = lerp1(sa.f, p00[k], p10[k]);
-      const float c2 = lerp1(sa.f, p00[k + 2], p10[k + 2]);
+      const float c1 = blend(sa.f, p0[k], p0[k + 2]);
+      const float c2 = blend(sa.f, p1[k], p1[k + 2]);
       AB13[k] = c1 + sb13.f * (c2 - c1);
     }
   }
   const Seg sb7 = bracket(BP_beta7_bp, T + OFF_pair_beta7, a.beta);
-  float AB7[4];
+  float AB7[4];  // Clda, Cldr, Cnda, Cndr over (alpha, beta 7)
   {
-    const float* p00 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 4;
-    const float* p10 = p00 + F16_N_B7 * 4;
+    const float* p0 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 8;
+    const float* p1 = p0 + 8;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float c1 = lerp1(sa.f, p00[k], p10[k]);
-      const float c2 = lerp1(sa.f, p00[k + 4], p10[k + 4]);
+      const float c1 = blend(sa.f, p0[k], p0[k + 4]);
+      const float c2 = blend(sa.f, p1[k], p1[k + 4]);
       AB7[k] = c1 + sb7.f * (c2 - c1);
     }
   }
-  // the nine mach tables on their union breakpoint grid, interleaved [13][9]
+  // the nine mach tables on their union breakpoint grid, [13][9 values | 9 mach-slopes]
   const Seg sm = bracket(BP_machu, T + OFF_pair_machu, a.mach);
   float MU[MACHU_NT];
   {
-    const float* r0 = T + OFF_machu_v + (sm.i - 1) * MACHU_NT;
-    const float* r1 = r0 + MACHU_NT;
+    const float* r0 = T + OFF_machu_v + (sm.i - 1) * (2 * MACHU_NT);
 #pragma unroll
-    for (int k = 0; k < MACHU_NT; ++k) MU[k] = lerp1(sm.f, r0[k], r1[k]);
+    for (int k = 0; k < MACHU_NT; ++k) MU[k] = blend(sm.f, r0[k], r0[MACHU_NT + k]);
   }
   const float CDmach = MU[MU_CDmach], CYb_M = MU[MU_CYb_M], Clb_M = MU[MU_Clb_M];
   const float Clda_M = MU[MU_Clda_M], Cldr_M = MU[MU_Cldr_M], Cma_M = MU[MU_Cma_M];
@@ -876,7 +898,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   ai.qbar = qbar; ai.alpha = alpha; ai.beta = beta; ai.mach = mach;
   ai.p = d.pqr[0]; ai.q = d.pqr[1]; ai.r = d.pqr[2];
   ai.bi2vel = bi2vel; ai.ci2vel = ci2vel;
-  ai.kclge = tab1(BP_kclge, T + OFF_pair_kclge, T + OFF_kclge_v, hbmac);
+  ai.kclge = tab1(BP_kclge, T + OFF_pair_kclge, T + OFF_kclge_vd, hbmac);
   ai.de = fc.de; ai.da = fc.da; ai.dr = fc.dr; ai.dlef = fc.dlef; ai.flap = fc.flap_mix; ai.dsb = fc.dsb;
   float A6[6];
   aero(ai, T, A6);

@@ -95,8 +95,17 @@ def test_oracle_tables_known_answers():
             assert L.f16ref_aero_table(k, xm, ym) == pytest.approx(want, abs=1e-12)
 
 
+def _slopes(v):
+    """slope[i] = f32(v[i+1]) - f32(v[i]) along axis 0 in fp32, 0 on the last row"""
+    v = np.asarray(v, np.float64).astype(np.float32)
+    d = np.zeros_like(v)
+    d[:-1] = v[1:] - v[:-1]
+    return v, d
+
+
 def test_kernel_blob_matches_fixture():
-    """The fp32 LDS blob in f16_tables.h holds exactly the fixture's tables (rounded to fp32)."""
+    """The fp32 LDS blob in f16_tables.h holds exactly the fixture's tables (rounded to fp32),
+    each beside its fp32 slope along the first interpolation axis (value, slope layout)."""
     m = model()
     src = open(os.path.join(ROOT, "f16_jsb_amd", "csrc", "f16_tables.h")).read()
     offs = {k: int(v) for k, v in re.findall(r"#define OFF_(\w+) (\d+)", src)}
@@ -105,21 +114,34 @@ def test_kernel_blob_matches_fixture():
     fns = {f["name"]: f for f in m["aero_functions"]}
     a1d = ["CDDlef", "CDDsb", "CDq", "CDq_Dlef", "CYp", "CYr", "CLDlef", "CLDsb", "CLq", "CLq_Dsb",
            "Clp", "Clr", "CmDsb", "Cmq", "Cnp", "Cnr"]
-    for j, n in enumerate(a1d):
-        got = blob[offs["alpha1d"] + np.arange(12) * 16 + j]
-        np.testing.assert_array_equal(got, np.float32(fns[n]["table"]["data"]))
-    for j, n in enumerate(["CDDh", "CLDh", "CmDh"]):
-        got = blob[offs["ade"] + np.arange(60) * 3 + j].reshape(12, 5)
-        np.testing.assert_array_equal(got, np.float32(fns[n]["table"]["data"]))
-    for j, n in enumerate(["Clb", "Cnb"]):
-        got = blob[offs["ab13"] + np.arange(156) * 2 + j].reshape(12, 13)
-        np.testing.assert_array_equal(got, np.float32(fns[n]["table"]["data"]))
-    for j, n in enumerate(["Clda", "Cldr", "Cnda", "Cndr"]):
-        got = blob[offs["ab7"] + np.arange(84) * 4 + j].reshape(12, 7)
-        np.testing.assert_array_equal(got, np.float32(fns[n]["table"]["data"]))
-    for n, t in m["engine"]["tables"].items():
-        got = blob[offs["eng_v_" + n]: offs["eng_v_" + n] + len(t["rows"]) * len(t["cols"])]
-        np.testing.assert_array_equal(got, np.float32(t["data"]).ravel())
+    for j, n in enumerate(a1d):  # [12][16 values | 16 slopes]
+        v, d = _slopes(fns[n]["table"]["data"])
+        np.testing.assert_array_equal(blob[offs["alpha1d"] + np.arange(12) * 32 + j], v)
+        np.testing.assert_array_equal(blob[offs["alpha1d"] + np.arange(12) * 32 + 16 + j], d)
+    for key, names, ncol in (("ade", ["CDDh", "CLDh", "CmDh"], 5), ("ab13", ["Clb", "Cnb"], 13),
+                             ("ab7", ["Clda", "Cldr", "Cnda", "Cndr"], 7)):
+        g = len(names)
+        for j, n in enumerate(names):  # [12][ncol][g values | g alpha-slopes]
+            v, d = _slopes(fns[n]["table"]["data"])
+            base = offs[key] + (np.arange(12)[:, None] * ncol + np.arange(ncol)[None, :]) * 2 * g
+            np.testing.assert_array_equal(blob[base + j], v)
+            np.testing.assert_array_equal(blob[base + g + j], d)
+    # engine: (mach x density-alt) union grid [14][8][3 values | 3 mach-slopes], Idle/Mil rows
+    # clamped at their last mach row
+    eng = m["engine"]["tables"]
+    rows = eng["AugThrust"]["rows"]
+    for j, n in enumerate(("IdleThrust", "MilThrust", "AugThrust")):
+        t = np.asarray(eng[n]["data"], np.float64)
+        full = t[np.minimum(np.arange(len(rows)), len(t) - 1)]
+        v, d = _slopes(full)
+        base = offs["engu_v"] + (np.arange(len(rows))[:, None] * 8 + np.arange(8)[None, :]) * 6
+        np.testing.assert_array_equal(blob[base + j], v)
+        np.testing.assert_array_equal(blob[base + 3 + j], d)
+    v, d = _slopes(m["kCLge"]["data"])
+    np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v))], v)
+    np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v)) + 1], d)
+    # (lo, 1/span) bracket pairs are 8-byte aligned for ds_read_b64
+    assert all(v % 2 == 0 for k, v in offs.items() if k.startswith("pair_") or k.endswith("_vd") or "_vd_" in k)
 
 
 # ------------------------------------------------------------------------------------------

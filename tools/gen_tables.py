@@ -24,6 +24,8 @@ import re
 import sys
 import xml.etree.ElementTree as ET
 
+import numpy as np
+
 REF = os.environ.get("F16_REFERENCE", "/root/reference")
 XML = os.path.join(REF, "aircraft/f16/f16.xml")
 ENG = os.path.join(REF, "aircraft/f16/Engines/F100-PW-229.xml")
@@ -302,35 +304,30 @@ def emit_kernel(model, path):
     listed = set(ALPHA_1D + ALPHA_DE_2D + ALPHA_BETA13 + ALPHA_BETA7 + MACH_1D)
     assert listed == {f["name"] for f in model["aero_functions"] if "table" in f}
 
-    put("alpha_bp", alpha_bp)
-    put("de_bp", de_bp)
-    put("beta13_bp", b13)
-    put("beta7_bp", b7)
-    # alpha-1D tables interleaved [12][16] so one alpha row is contiguous
-    put("alpha1d", [fns[n]["table"]["data"][i] for i in range(12) for n in ALPHA_1D])
-    # 2-D (alpha x de): [12][5][3]
-    put("ade", [fns[n]["table"]["data"][i][j] for i in range(12) for j in range(5) for n in ALPHA_DE_2D])
-    put("ab13", [fns[n]["table"]["data"][i][j] for i in range(12) for j in range(13) for n in ALPHA_BETA13])
-    put("ab7", [fns[n]["table"]["data"][i][j] for i in range(12) for j in range(7) for n in ALPHA_BETA7])
-    mach_meta = []
-    for n in MACH_1D:
-        t = fns[n]["table"]
-        put("mach_bp_" + n, t["rows"])
-        put("mach_v_" + n, t["data"])
-        mach_meta.append((n, len(t["rows"])))
-    put("kclge_bp", model["kCLge"]["rows"])
-    put("kclge_v", model["kCLge"]["data"])
-    for n, t in model["fcs_tables"].items():
-        k = n.split("/")[-1]
-        put("fcs_bp_" + k, t["rows"])
-        put("fcs_v_" + k, t["data"])
-    eng_meta = []
-    for n in ("IdleThrust", "MilThrust", "AugThrust"):
-        t = model["engine"]["tables"][n]
-        put("eng_r_" + n, t["rows"])
-        put("eng_c_" + n, t["cols"])
-        put("eng_v_" + n, [v for r in t["data"] for v in r])
-        eng_meta.append((n, len(t["rows"]), len(t["cols"])))
+    # Every table is stored as (value, slope) along the interpolation axis the kernel blends
+    # first: slope[i] = f32(v[i+1]) - f32(v[i]) (fp32 arithmetic, 0 on the last row), so a
+    # lerp is one FMA v + f * slope -- bit-identical to f * (v1 - v0) + v0 computed in-kernel.
+    def put_rows(key, rows_vals, group):
+        """rows over the interpolation axis, each a list of entries of `group` values; emitted
+        per (row, entry) as the group's values then its slopes"""
+        v = [np.array(r, np.float64).astype(np.float32) for r in rows_vals]
+        vals = []
+        for i in range(len(v)):
+            d = (v[i + 1] - v[i]) if i + 1 < len(v) else np.zeros_like(v[i])
+            for e in range(len(v[i]) // group):
+                vals += [float(x) for x in v[i][e * group:(e + 1) * group]]
+                vals += [float(x) for x in d[e * group:(e + 1) * group]]
+        put(key, vals)
+
+    # alpha-1D tables: [12 alpha][16 values | 16 slopes]
+    put_rows("alpha1d", [[fns[n]["table"]["data"][i] for n in ALPHA_1D] for i in range(12)], len(ALPHA_1D))
+    # 2-D over (alpha, X): [12 alpha][X][group values | group alpha-slopes]
+    put_rows("ade", [[fns[n]["table"]["data"][i][j] for j in range(len(de_bp)) for n in ALPHA_DE_2D]
+                     for i in range(12)], len(ALPHA_DE_2D))
+    put_rows("ab13", [[fns[n]["table"]["data"][i][j] for j in range(len(b13)) for n in ALPHA_BETA13]
+                      for i in range(12)], len(ALPHA_BETA13))
+    put_rows("ab7", [[fns[n]["table"]["data"][i][j] for j in range(len(b7)) for n in ALPHA_BETA7]
+                     for i in range(12)], len(ALPHA_BETA7))
 
     # ---- union grids (exact re-gridding: every original breakpoint is a union breakpoint,
     # so the piecewise-linear, end-clamped functions are unchanged up to fp rounding) -------
@@ -346,8 +343,9 @@ def emit_kernel(model, path):
         return data[i - 1] + f * (data[i] - data[i - 1])
 
     mach_u = sorted({b for n in MACH_1D for b in fns[n]["table"]["rows"]})
-    put("machu_v", [interp_clamped(fns[n]["table"]["rows"], fns[n]["table"]["data"], x)
-                    for x in mach_u for n in MACH_1D])
+    # [13 mach][9 values | 9 slopes]
+    put_rows("machu_v", [[interp_clamped(fns[n]["table"]["rows"], fns[n]["table"]["data"], x) for n in MACH_1D]
+                         for x in mach_u], len(MACH_1D))
     eng_rows = model["engine"]["tables"]["AugThrust"]["rows"]
     eng_cols = model["engine"]["tables"]["AugThrust"]["cols"]
     eng_names = ("IdleThrust", "MilThrust", "AugThrust")
@@ -357,12 +355,19 @@ def emit_kernel(model, path):
         assert t["rows"] == eng_rows[:len(t["rows"])]
     eng_u = []
     for i in range(len(eng_rows)):
+        row = []
         for j in range(len(eng_cols)):
             for n in eng_names:
                 t = model["engine"]["tables"][n]
                 ii = min(i, len(t["rows"]) - 1)  # FGTable clamps the row factor at the last row
-                eng_u.append(t["data"][ii][j])
-    put("engu_v", eng_u)
+                row.append(t["data"][ii][j])
+        eng_u.append(row)
+    # [14 mach][8 density-alt][3 values | 3 mach-slopes]
+    put_rows("engu_v", eng_u, len(eng_names))
+    # small 1-D tables: (value, slope) pairs
+    put_rows("kclge_vd", [[v] for v in model["kCLge"]["data"]], 1)
+    for n, t in model["fcs_tables"].items():
+        put_rows("fcs_vd_" + n.split("/")[-1], [[v] for v in t["data"]], 1)
     # (lo, 1/span) pairs for LDS brackets (8-byte aligned for ds_read_b64)
     while len(blob) % 4:  # whole 16-byte pieces: the kernels stage the blob by LDS-DMA
         blob.append(0.0)
@@ -379,6 +384,9 @@ def emit_kernel(model, path):
         put("pair_fcs_" + n.split("/")[-1], pairs(t["rows"]))
     while len(blob) % 4:  # whole 16-byte pieces: the kernels stage the blob by LDS-DMA
         blob.append(0.0)
+    mach_meta = [(n, len(fns[n]["table"]["rows"])) for n in MACH_1D]
+    eng_meta = [(n, len(model["engine"]["tables"][n]["rows"]), len(model["engine"]["tables"][n]["cols"]))
+                for n in eng_names]
 
     L = ["/* GENERATED by tools/gen_tables.py from the reference's f16.xml / F100-PW-229.xml.",
          " * fp32 table blob staged into LDS by the step kernel. Do not edit by hand. */",
@@ -417,11 +425,10 @@ def emit_kernel(model, path):
     L.append("")
     L.append("/* breakpoint vectors are also emitted as constexpr arrays so unrolled searches fold")
     L.append(" * them into instruction literals (no LDS reads for breakpoints). */")
-    for key in ("alpha_bp", "de_bp", "beta13_bp", "beta7_bp"):
-        n = {"alpha_bp": len(alpha_bp), "de_bp": len(de_bp), "beta13_bp": len(b13), "beta7_bp": len(b7)}[key]
-        L.append("static constexpr float BP_%s[%d] = {%s};" % (key, n, ", ".join(_lit(v, "%.9gf") for v in blob[offs[key]:offs[key] + n])))
+    for key, bp in (("alpha_bp", alpha_bp), ("de_bp", de_bp), ("beta13_bp", b13), ("beta7_bp", b7)):
+        L.append("static constexpr float BP_%s[%d] = {%s};" % (key, len(bp), ", ".join(_lit(v, "%.9gf") for v in bp)))
     for n, nr in mach_meta:
-        L.append("static constexpr float BP_mach_%s[%d] = {%s};" % (n, nr, ", ".join(_lit(v, "%.9gf") for v in blob[offs["mach_bp_" + n]:offs["mach_bp_" + n] + nr])))
+        L.append("static constexpr float BP_mach_%s[%d] = {%s};" % (n, nr, ", ".join(_lit(v, "%.9gf") for v in fns[n]["table"]["rows"])))
     L.append("static constexpr float BP_kclge[%d] = {%s};" % (len(model["kCLge"]["rows"]), ", ".join(_lit(v, "%.9gf") for v in model["kCLge"]["rows"])))
     for n, t in model["fcs_tables"].items():
         L.append("static constexpr float BP_fcs_%s[%d] = {%s};" % (_cname(n.split("/")[-1]), len(t["rows"]), ", ".join(_lit(v, "%.9gf") for v in t["rows"])))

@@ -37,10 +37,10 @@ def classify(op: str) -> str:
 
 
 def main():
-    flags = [a for a in sys.argv[1:] if a.startswith("-D")]
+    flags = [a for a in sys.argv[1:] if a.startswith(("-D", "-f"))]
     kernel = "_Z15f16_step_kernel8StepArgs"
     dump = None
-    args = [a for a in sys.argv[1:] if not a.startswith("-D")]
+    args = [a for a in sys.argv[1:] if not a.startswith(("-D", "-f"))]
     for i, a in enumerate(args):
         if a == "--kernel":
             kernel = args[i + 1]
