@@ -148,6 +148,29 @@ def rollout_bench(args, dev, rank, world):
     return r
 
 
+def features_bench(envs, stream, iters=200):
+    """SURVEY 8f rank 3 beside the headline: the policy feature transform (features.py:37-67,
+    15 -> 17 floats per frame) over the env's (N, K, 15) device obs; HBM-bound, 128 B/frame."""
+    import torch
+    from f16_jsb_amd.features import features
+    obs = envs.obs
+    out = torch.empty(obs.shape[:-1] + (17,), dtype=torch.float32, device=obs.device)
+    for _ in range(10):
+        features(obs, out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(iters):
+        features(obs, out)
+    e.record(stream)
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    frames = obs.numel() // 15
+    gbps = frames * (15 + 17) * 4 / (ms * 1e-3) / 1e9
+    return {"kernel": "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
+            "frames_per_s": round(frames / (ms * 1e-3), 1), "achieved_GBps": round(gbps, 1),
+            "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128}
+
+
 def load_traffic(envs, stack, state_bytes):
     """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if it was
     measured on this workload and state layout."""
@@ -232,6 +255,7 @@ def main():
     durs = sorted(s.elapsed_time(e) for s, e in ev)
     kern_ms = durs[len(durs) // 2]
     done_frac = float(((envs.term | envs.trunc).sum()).item()) / n
+    feat = features_bench(envs, stream)
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -297,6 +321,7 @@ def main():
             "launch_env_steps": n,
         },
         "done_fraction_last_step": round(done_frac, 5),
+        "features": feat,
     }
     if rollout is not None:
         out["rollout"] = rollout

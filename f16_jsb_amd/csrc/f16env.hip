@@ -893,6 +893,66 @@ __global__ void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __r
   }
 }
 
+// Per-frame policy features: jsbsim_gym/features.py:37-67
+// JSBSimFeatureExtractor.forward, 15 observation floats -> 17 features, float32 throughout
+// (torch float32 semantics: IEEE division / sqrt, ~1-ulp atan2 / cos / sin), applied to every
+// frame of a (..., 15) block, e.g. the (N, K, 15) stack as the first stage of
+// LMA_features.py:744-776 StackedLMAFeaturesExtractor does. HBM-bound (60 B in, 68 B out per
+// frame): each 256-thread block moves its 256 frames as coalesced float4 through LDS (frame
+// strides 15 and 17 are odd, so the per-thread LDS reads/writes are bank-conflict free).
+#define FEAT_IN 15
+#define FEAT_OUT 17
+__global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, const float* __restrict__ obs,
+                                                           float* __restrict__ feat) {
+  __shared__ __align__(16) float sIn[256 * FEAT_IN];
+  __shared__ __align__(16) float sOut[256 * FEAT_OUT];
+  const int64_t f0 = (int64_t)blockIdx.x * 256;
+  const int nf = (int)(n_frames - f0 < 256 ? n_frames - f0 : 256);
+  const int t = threadIdx.x;
+  const float* gin = obs + f0 * FEAT_IN;
+  float* gout = feat + f0 * FEAT_OUT;
+  // whole-block float4 moves need 16-byte alignment of the block's slice (base % 16 == 0 and
+  // a full block: 256 * 15 * 4 and 256 * 17 * 4 bytes are multiples of 16)
+  const bool vin = nf == 256 && (((uintptr_t)gin) & 15) == 0;
+  const bool vout = nf == 256 && (((uintptr_t)gout) & 15) == 0;
+  if (vin) {
+    for (int q = t; q < 256 * FEAT_IN / 4; q += 256)
+      reinterpret_cast<float4*>(sIn)[q] = reinterpret_cast<const float4*>(gin)[q];
+  } else {
+    for (int q = t; q < nf * FEAT_IN; q += 256) sIn[q] = gin[q];
+  }
+  __syncthreads();
+  if (t < nf) {
+#pragma clang fp contract(off)  // torch float32: every product and sum rounded separately
+    const float* o = sIn + t * FEAT_IN;
+    float* y = sOut + t * FEAT_OUT;
+    // features.py:39-45 unpack; :47-53 position transform
+    const float dx = o[12] - o[0], dy = o[13] - o[1], dz = o[14] - o[2];
+    float d2 = dx * dx;
+    d2 = __fadd_rn(d2, __fmul_rn(dy, dy));
+    const float distance = __fsqrt_rn(d2);
+    const float abs_bearing = atan2f(dy, dx);
+    const float rel_bearing = abs_bearing - o[11];
+    y[0] = __fdiv_rn(1.0f, __fadd_rn(1.0f, __fmul_rn(distance, 1e-3f)));  // :56 dist_norm
+    y[1] = __fdiv_rn(dz, 15000.0f);                                         // :59 dz_norm
+    y[2] = __fdiv_rn(o[2], 15000.0f);                                       // :60 alt_norm
+    y[3] = o[3];                                                            // mach
+    y[4] = o[6]; y[5] = o[7]; y[6] = o[8];                                  // angular rates
+    y[7] = cosf(o[4]); y[8] = cosf(o[5]);                                   // :63 cos(alpha, beta)
+    y[9] = sinf(o[4]); y[10] = sinf(o[5]);                                  //     sin(alpha, beta)
+    y[11] = cosf(o[9]); y[12] = cosf(o[10]);                                // :64 cos(phi, theta)
+    y[13] = sinf(o[9]); y[14] = sinf(o[10]);                                //     sin(phi, theta)
+    y[15] = cosf(rel_bearing); y[16] = sinf(rel_bearing);                   // :65
+  }
+  __syncthreads();
+  if (vout) {
+    for (int q = t; q < 256 * FEAT_OUT / 4; q += 256)
+      reinterpret_cast<float4*>(gout)[q] = reinterpret_cast<const float4*>(sOut)[q];
+  } else {
+    for (int q = t; q < nf * FEAT_OUT; q += 256) gout[q] = sOut[q];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -1200,6 +1260,19 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
   const float g = (float)gamma, gl = (float)(gamma * gae_lambda);
   hipLaunchKernelGGL(f16_gae_kernel, dim3((unsigned)((n_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      n_steps, n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_features(void* stream, int64_t n_frames, const float* obs, float* feat) {
+  if (n_frames < 0) return set_err(-1, "n_frames must be >= 0");
+  if (n_frames == 0) return 0;
+  if (!obs || !feat) return set_err(-1, "null argument");
+  if (((uintptr_t)obs & 3) != 0 || ((uintptr_t)feat & 3) != 0) return set_err(-1, "obs and feat must be float-aligned");
+  const int64_t blocks = (n_frames + 255) / 256;
+  if (blocks > 0x7fffffffLL) return set_err(-1, "n_frames too large");
+  hipLaunchKernelGGL(f16_features_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_frames, obs,
+                     feat);
   HIPCHK(hipGetLastError());
   return 0;
 }

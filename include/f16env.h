@@ -21,6 +21,8 @@
  *                      parity replay and checkpoint/restore)
  *   f16env_trim     <- no reference equivalent (the reference never trims; BASELINE cfg 2)
  *   f16env_sample_actions <- action_space.sample() (jsbsim_gym.py:575), device Philox
+ *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
+ *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
  */
 #ifndef F16ENV_H
 #define F16ENV_H
@@ -205,6 +207,15 @@ int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step
 int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
                const float* episode_starts, const float* last_values, const uint8_t* dones, double gamma,
                double gae_lambda, float* advantages, float* returns);
+
+/* Policy features of every observation frame, replacing
+ * jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (float32):
+ *   obs  n_frames x 15 float (any (..., 15) block, e.g. the N x K x 15 stack)
+ *   feat n_frames x 17 float: [1/(1+d/1000), dz/15000, h/15000, mach, p, q, r,
+ *        cos a, cos b, sin a, sin b, cos phi, cos theta, sin phi, sin theta, cos rb, sin rb]
+ *        with d = |goal - pos|_xy, dz = goal_z - h, rb = atan2(dy, dx) - psi.
+ * No handle needed; stream-ordered. */
+int f16env_features(void* stream, int64_t n_frames, const float* obs, float* feat);
 
 /* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
  * HBM bytes one env-step moves. */
