@@ -77,7 +77,20 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
         if el >= seconds or steps >= 2000:
             break
     e.close()
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+    # BASELINE cfg1 semantics beside it: ONE env, 1000 random-action steps, reference stack K=10
+    e1 = OracleEnvs(1, stack_k=10, seed=1)
+    e1.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform([-1, -1, -1, 0], [1, 1, 1, 1], (1000, 1, 4)).astype(np.float32)
+    t1 = time.perf_counter()
+    for t in range(1000):
+        e1.step(acts[t])
+    el1 = time.perf_counter() - t1
+    e1.close()
+    cfg1 = {"value": round(1000 / el1, 1), "unit": "env-steps/s", "cores": 1,
+            "sample": "BASELINE cfg1: 1 env x 1000 random-action steps (numpy default_rng(0), K=10), "
+                      "oracle/f16ref.c through its ctypes step (one env, no parallelism)"}
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port", "cfg1": cfg1,
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
                       "%d envs x %d random-action steps (stack=%d, auto-reset%s), %d OpenMP threads, %.1f s"
                       % (n, steps, stack, ", cfg5 random IC + gusts" if cfg5 else "", threads, el)}

@@ -288,3 +288,35 @@ def test_trimmed_flight_is_level():
         obs, *_ = e.step(act)
     assert abs(obs[0, -1, 2] - h0) < 30.0
     assert abs(obs[0, -1, 3] - m0) < 0.01
+
+
+def test_cfg1_single_env_1000_random_steps():
+    """BASELINE cfg1: 1 env, reference IC, 1000 steps of Box-uniform random actions
+    from numpy.random.default_rng(0) (jsbsim_gym.py:143-148 bounds), first reset seed 0
+    (jsbsim_gym.py:312-323 goal), through the CPU oracle: finite observations inside the
+    float32 frame format, the step counter / Monitor length bookkeeping across auto-resets,
+    and returns equal to the sum of the step rewards."""
+    from f16_jsb_amd.env import reference_goal
+    e = OracleEnvs(1, stack_k=10)
+    obs = e.reset(goals=reference_goal(0)[None, :])
+    np.testing.assert_array_equal(obs[0, -1, 12:], reference_goal(0))
+    rng = np.random.default_rng(0)
+    low, high = np.array([-1, -1, -1, 0], np.float32), np.array([1, 1, 1, 1], np.float32)
+    ep_len, ep_ret, episodes = 0, 0.0, 0
+    for t in range(1000):
+        a = rng.uniform(low, high).astype(np.float32)[None, :]
+        obs, rew, term, trunc, tobs, eret, elen = e.step(a)
+        assert obs.shape == (1, 10, 15) and obs.dtype == np.float32 and np.all(np.isfinite(obs))
+        ep_len += 1
+        ep_ret += float(rew[0])
+        assert not (term[0] and trunc[0])
+        if term[0] or trunc[0]:
+            episodes += 1
+            assert elen[0] == ep_len and trunc[0] == (ep_len >= 1200)
+            assert eret[0] == pytest.approx(ep_ret, abs=1e-3)
+            assert np.all(obs[0] == obs[0, 0])  # K copies of the reset frame
+            ep_len, ep_ret = 0, 0.0
+        else:
+            # attitude angles normalised to [-pi, pi) (jsbsim_gym.py:186-188)
+            assert np.all(np.abs(obs[0, -1, 9:12]) <= np.float32(np.pi))
+    assert episodes + (ep_len > 0) >= 1
