@@ -261,6 +261,13 @@ __device__ __forceinline__ float fatan2(float y, float x) {
 // blend with a precomputed slope: v + f (v_next - v), the slope stored beside the value in
 // the blob (tools/gen_tables.py), i.e. the same fp32 FMA as lerp1 without the subtraction
 __device__ __forceinline__ float blend(float f, float v, float slope) { return __builtin_fmaf(f, slope, v); }
+// the same on two tables at once (v_pk_fma_f32: two fp32 FMAs per lane per instruction, the
+// factor broadcast by op_sel); values/slopes come from LDS as register pairs
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v ld2(const float* p) { return f2v{p[0], p[1]}; }
+__device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
+  return __builtin_elementwise_fma(f2v{f, f}, slope, v);
+}
 
 // 1-D lookup: literal breakpoints, LDS (lo, 1/span) pairs, LDS (value, slope) pairs
 template <int N>
@@ -673,11 +680,12 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   const float* e00 = T + OFF_engu_v + ((er.i - 1) * ENGU_NC + ec.i - 1) * 6;
   const float* e01 = e00 + 6;
   float ev[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float c1 = blend(er.f, e00[k], e00[k + 3]);
-    const float c2 = blend(er.f, e01[k], e01[k + 3]);
-    ev[k] = c1 + ec.f * (c2 - c1);
+  {
+    const f2v c1 = blend2(er.f, ld2(e00), ld2(e00 + 3)), c2 = blend2(er.f, ld2(e01), ld2(e01 + 3));
+    const f2v r = blend2(ec.f, c1, c2 - c1);
+    ev[0] = r.x; ev[1] = r.y;
+    const float d1 = blend(er.f, e00[2], e00[5]), d2 = blend(er.f, e01[2], e01[5]);
+    ev[2] = d1 + ec.f * (d2 - d1);
   }
   const float idle = 17800.0f * ev[0];
   const float mil = (17800.0f - idle) * ev[1];
@@ -718,7 +726,11 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   {
     const float* r0 = T + OFF_alpha1d + (sa.i - 1) * (2 * F16_N_A1D);
 #pragma unroll
-    for (int k = 0; k < F16_N_A1D; ++k) A[k] = blend(sa.f, r0[k], r0[F16_N_A1D + k]);
+    for (int k = 0; k < F16_N_A1D / 2; ++k) {
+      const f2v r = blend2(sa.f, ld2(r0 + 2 * k), ld2(r0 + F16_N_A1D + 2 * k));
+      A[2 * k] = r.x;
+      A[2 * k + 1] = r.y;
+    }
   }
   // 2-D over (alpha, X), entries [12][X][G values | G alpha-slopes]: blend along alpha at the
   // two bracketing X columns, then along X
@@ -727,24 +739,20 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   {
     const float* p0 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 6;
     const float* p1 = p0 + 6;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float c1 = blend(sa.f, p0[k], p0[k + 3]);
-      const float c2 = blend(sa.f, p1[k], p1[k + 3]);
-      ADE[k] = c1 + se.f * (c2 - c1);
-    }
+    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 3)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 3));
+    const f2v r = blend2(se.f, c1, c2 - c1);
+    ADE[0] = r.x; ADE[1] = r.y;
+    const float d1 = blend(sa.f, p0[2], p0[5]), d2 = blend(sa.f, p1[2], p1[5]);
+    ADE[2] = d1 + se.f * (d2 - d1);
   }
   const Seg sb13 = bracket(BP_beta13_bp, T + OFF_pair_beta13, a.beta);
   float AB13[2];  // Clb, Cnb over (alpha, beta 13)
   {
     const float* p0 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 4;
     const float* p1 = p0 + 4;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const float c1 = blend(sa.f, p0[k], p0[k + 2]);
-      const float c2 = blend(sa.f, p1[k], p1[k + 2]);
-      AB13[k] = c1 + sb13.f * (c2 - c1);
-    }
+    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 2)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 2));
+    const f2v r = blend2(sb13.f, c1, c2 - c1);
+    AB13[0] = r.x; AB13[1] = r.y;
   }
   const Seg sb7 = bracket(BP_beta7_bp, T + OFF_pair_beta7, a.beta);
   float AB7[4];  // Clda, Cldr, Cnda, Cndr over (alpha, beta 7)
@@ -752,10 +760,10 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     const float* p0 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 8;
     const float* p1 = p0 + 8;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float c1 = blend(sa.f, p0[k], p0[k + 4]);
-      const float c2 = blend(sa.f, p1[k], p1[k + 4]);
-      AB7[k] = c1 + sb7.f * (c2 - c1);
+    for (int k = 0; k < 4; k += 2) {
+      const f2v c1 = blend2(sa.f, ld2(p0 + k), ld2(p0 + k + 4)), c2 = blend2(sa.f, ld2(p1 + k), ld2(p1 + k + 4));
+      const f2v r = blend2(sb7.f, c1, c2 - c1);
+      AB7[k] = r.x; AB7[k + 1] = r.y;
     }
   }
   // the nine mach tables on their union breakpoint grid, [13][9 values | 9 mach-slopes]
@@ -764,7 +772,11 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   {
     const float* r0 = T + OFF_machu_v + (sm.i - 1) * (2 * MACHU_NT);
 #pragma unroll
-    for (int k = 0; k < MACHU_NT; ++k) MU[k] = blend(sm.f, r0[k], r0[MACHU_NT + k]);
+    for (int k = 0; k + 1 < MACHU_NT; k += 2) {
+      const f2v r = blend2(sm.f, ld2(r0 + k), ld2(r0 + MACHU_NT + k));
+      MU[k] = r.x; MU[k + 1] = r.y;
+    }
+    if (MACHU_NT & 1) MU[MACHU_NT - 1] = blend(sm.f, r0[MACHU_NT - 1], r0[2 * MACHU_NT - 1]);
   }
   const float CDmach = MU[MU_CDmach], CYb_M = MU[MU_CYb_M], Clb_M = MU[MU_Clb_M];
   const float Clda_M = MU[MU_Clda_M], Cldr_M = MU[MU_Cldr_M], Cma_M = MU[MU_Cma_M];
