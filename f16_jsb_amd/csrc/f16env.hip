@@ -347,8 +347,12 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // MODE bit 0: F16_FLAG_RANDOM_IC, bit 1: F16_FLAG_GUSTS. MODE 0 (the reference's task) resets
 // finished lanes inline from the IC template; other modes leave finished lanes to
 // f16_reset_done_kernel (a full RunIC per lane is too long to run divergently in-wave).
-template <int MODE>
-__device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* sTmpl, int* sDone, float* dynl) {
+// GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
+// frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
+// 160 KB). sT is then unused.
+template <int MODE, bool GT = false>
+__device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
+  const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
 #ifdef F16_STAMPS
   Stamps stamps = {};
@@ -385,7 +389,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
   // action), then one wait: a single HBM round trip before the physics. The previous stack
   // (only needed by the obs rebuild) is DMA'd after that wait, so it streams in while the
   // first frame runs instead of sharing the prologue's HBM bandwidth.
-  stage_tables_issue(sT);
+  if (!GT) stage_tables_issue(sT_lds);
   if (!DEFER && threadIdx.x < NCOL) dma16(reinterpret_cast<const float*>(a.tmpl.c + threadIdx.x),
                                           reinterpret_cast<float*>(sTmpl));
   if (live) {
@@ -558,7 +562,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT, float4* 
       float* tout = a.tobs ? a.tobs + row0 * KC : nullptr;
       const int total = rows * KC;
       int row = lane / KC, col = lane - (lane / KC) * KC;
-      constexpr int CH = 16;
+#ifndef F16_FALLBACK_CH
+#define F16_FALLBACK_CH 16
+#endif
+      constexpr int CH = F16_FALLBACK_CH;
       for (int base = 0; base < total; base += 64 * CH) {
         float v[CH];
         int rw[CH], cl[CH];
@@ -620,12 +627,22 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
   STEP_SHARED
   step_body<MODE>(a, sT, sTmpl, sDone, dynl);
 }
+// global-table variant (large K on the LDS-image path): no LDS table copy
+template <int MODE>
+__global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
+  __shared__ __align__(16) float4 sTmpl[NCOL];
+  __shared__ int sDone[BLOCK];
+  extern __shared__ __align__(16) float dynl[];
+  step_body<MODE, true>(a, nullptr, sTmpl, sDone, dynl);
+}
 using StepKernel = void (*)(StepArgs);
-static StepKernel step_kernel_for(int mode, int occ) {
-  static const StepKernel table[2][4] = {
+// variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables
+static StepKernel step_kernel_for(int mode, int variant) {
+  static const StepKernel table[3][4] = {
       {f16_step_kernel, f16_step_var_kernel<1, 1>, f16_step_var_kernel<2, 1>, f16_step_var_kernel<3, 1>},
-      {f16_step_var_kernel<0, 2>, f16_step_var_kernel<1, 2>, f16_step_var_kernel<2, 2>, f16_step_var_kernel<3, 2>}};
-  return table[occ == 2 ? 1 : 0][mode & 3];
+      {f16_step_var_kernel<0, 2>, f16_step_var_kernel<1, 2>, f16_step_var_kernel<2, 2>, f16_step_var_kernel<3, 2>},
+      {f16_step_gt_kernel<0>, f16_step_gt_kernel<1>, f16_step_gt_kernel<2>, f16_step_gt_kernel<3>}};
+  return table[variant < 0 || variant > 2 ? 0 : variant][mode & 3];
 }
 
 // cfg5 auto-reset of the lanes a deferred-mode step finished (done list from its ballot
@@ -969,6 +986,7 @@ struct f16env {
   ModelConsts C;
   size_t bytes;
   int lds_image;   // step kernel stack-rebuild mode (LDS image when it fits)
+  int gt;          // 1: the global-table step kernel (the image needs all of LDS, large K)
   size_t dyn_lds;  // dynamic LDS bytes per step-kernel block
 };
 
@@ -1126,20 +1144,31 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const int KC = cfg->stack_k * F16_OBS_DIM;
     const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
     const size_t fallback = sizeof(float) * 2 * BLOCK * FRAME_PITCH;
-    const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + 16 * NCOL + sizeof(int) * BLOCK + 64;
-    h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : 0;
+    const size_t static_gt = 16 * NCOL + sizeof(int) * BLOCK + 64;
+    const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + static_gt;
+    // the stack image with LDS tables if both fit, else with global tables, else the
+    // chunked flat copy (LDS tables)
+    h->lds_image = (img + static_lds <= 160 * 1024) ? 1 : (img + static_gt <= 160 * 1024 ? 1 : 0);
+    h->gt = (h->lds_image && img + static_lds > 160 * 1024) ? 1 : 0;
+    if (getenv("F16ENV_GT") && h->lds_image) h->gt = atoi(getenv("F16ENV_GT")) ? 1 : 0;
     h->dyn_lds = h->lds_image ? img : fallback;
-    for (int occ = 1; occ <= 2; ++occ)
+    for (int v = 0; v <= 2; ++v) {
+      if ((v == 2 ? static_gt : static_lds) + h->dyn_lds > 160 * 1024) continue;  // not launchable here
       for (int m = 0; m < 4; ++m)
-        hipFuncSetAttribute((const void*)step_kernel_for(m, occ), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)h->dyn_lds);
+        if (hipFuncSetAttribute((const void*)step_kernel_for(m, v), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)h->dyn_lds) != hipSuccess) {
+          (void)hipGetLastError();
+          hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
+          return set_err(-2, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        }
+    }
     // two waves per SIMD only pay when there are more waves than SIMDs and two workgroups'
     // LDS (tables + stack image) fit in one CU
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
       cus = 256;
     const int64_t waves = ((int64_t)cfg->n_envs + 63) / 64;
-    h->occ = (waves > 4 * (int64_t)cus && 2 * (static_lds + h->dyn_lds) <= 160 * 1024) ? 2 : 1;
+    h->occ = (!h->gt && waves > 4 * (int64_t)cus && 2 * (static_lds + h->dyn_lds) <= 160 * 1024) ? 2 : 1;
     if (getenv("F16ENV_OCC")) h->occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
   }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
@@ -1207,7 +1236,7 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
   }
   if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  hipLaunchKernelGGL(step_kernel_for(h->mode, h->occ), grid, blk, h->dyn_lds, st, a);
+  hipLaunchKernelGGL(step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0)), grid, blk, h->dyn_lds, st, a);
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
@@ -1279,6 +1308,7 @@ int f16env_features(void* stream, int64_t n_frames, const float* obs, float* fea
 
 const char* f16env_step_kernel_name(void) { return "f16_step_kernel"; }
 int f16env_step_waves_per_simd(f16env_t h) { return h ? h->occ : 0; }
+int f16env_step_variant(f16env_t h) { return h ? (h->gt ? 2 : (h->occ == 2 ? 1 : 0)) : -1; }
 
 double f16env_algorithmic_bytes_per_env_step(int stack_k) {
   return 16.0 + 60.0 * stack_k + 60.0 * (stack_k - 1) + 4.0 + 2.0 + 2.0 * STATE_BYTES;

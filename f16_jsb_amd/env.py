@@ -108,7 +108,10 @@ class F16Envs:
     @property
     def step_kernel_name(self) -> str:
         mode = (1 if self.cfg.flags & F16_FLAG_RANDOM_IC else 0) | (2 if self.cfg.flags & F16_FLAG_GUSTS else 0)
-        occ = self.waves_per_simd
+        variant = int(lib().f16env_step_variant(self._h))
+        if variant == 2:
+            return "f16_step_gt_kernel<%d>" % mode
+        occ = 2 if variant == 1 else 1
         return "f16_step_kernel" if (mode, occ) == (0, 1) else "f16_step_var_kernel<%d, %d>" % (mode, occ)
 
     @property

@@ -223,6 +223,10 @@ const char* f16env_step_kernel_name(void);
 /* Waves per SIMD the handle's step kernel is built for: 1 (up to 64 x 4 x CUs envs), or 2
  * when there are more waves than SIMDs (override: env F16ENV_OCC=1|2 at create). */
 int f16env_step_waves_per_simd(f16env_t h);
+/* Step kernel variant of the handle: 0 = tables in LDS, one wave per SIMD; 1 = tables in LDS,
+ * two waves per SIMD; 2 = tables read from global memory (L1/L2) so that the K-frame stack
+ * image alone fills LDS (large K, e.g. the reference's K = 10; override: env F16ENV_GT=0|1). */
+int f16env_step_variant(f16env_t h);
 double f16env_algorithmic_bytes_per_env_step(int stack_k);
 
 const char* f16env_last_error(void);

@@ -303,3 +303,30 @@ def test_vecenv_sb3_contract(torch_mod):
             total += 1
     assert total >= n  # every lane finished at least once (crash / goal / 1200-step truncation)
     env.close()
+
+
+def test_global_table_variant_bit_identical(torch_mod, monkeypatch):
+    """The global-table step kernel (chosen when the K-frame stack image fills LDS, e.g. the
+    reference's K = 10) runs the same arithmetic as the LDS-table kernel: forced on a K = 4
+    handle (F16ENV_GT=1) it must reproduce the default handle bit for bit, and at K = 10 it
+    is the variant the handle picks."""
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    n = 3000
+    a = F16Envs(n, stack_k=4, seed=5)
+    monkeypatch.setenv("F16ENV_GT", "1")
+    b = F16Envs(n, stack_k=4, seed=5)
+    monkeypatch.delenv("F16ENV_GT")
+    assert a.step_kernel_name == "f16_step_kernel" and b.step_kernel_name.startswith("f16_step_gt_kernel")
+    a.reset()
+    b.reset()
+    for t in range(60):
+        act = a.sample_actions(11, t)
+        oa, ob = a.step(act), b.step(act)
+        assert torch.equal(oa.obs, ob.obs) and torch.equal(oa.rew, ob.rew)
+        assert torch.equal(oa.terminated, ob.terminated) and torch.equal(oa.truncated, ob.truncated)
+    assert torch.equal(a.get_state(), b.get_state())
+    c = F16Envs(256, stack_k=10, seed=5)
+    assert c.step_kernel_name.startswith("f16_step_gt_kernel")
+    for h in (a, b, c):
+        h.close()

@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PAT = os.path.join(ROOT, "f16_jsb_amd", "libf16env_var_%s.so")
-CASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4)]
+CASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4), (65536, 10, 4), (4096, 4, 4)]
 
 
 def build(specs):
