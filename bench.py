@@ -184,6 +184,31 @@ def features_bench(envs, stream, iters=200):
             "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128}
 
 
+def sb3_compat_bench(dev, n, steps=20):
+    """SURVEY 8d 'also reported': the SB3 drop-in mode -- F16VecEnv with numpy returns and the
+    per-env infos list (dummy_vec_env.py:56-73 semantics), at the reference's stack K=10 --
+    timed at the VecEnv boundary including the device->host copies and the Python infos."""
+    import numpy as np
+    import torch
+    from f16_jsb_amd.env import F16VecEnv
+    venv = F16VecEnv(num_envs=n, stack_k=10, device=dev, seed=5, return_numpy=True)
+    venv.reset()
+    rng = np.random.default_rng(0)
+    acts = [torch.as_tensor(rng.uniform([-1, -1, -1, 0], [1, 1, 1, 1], (n, 4)).astype(np.float32), device=dev)
+            for _ in range(4)]
+    for t in range(3):
+        venv.step(acts[t % 4])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        obs, rew, dones, infos = venv.step(acts[t % 4])
+    el = time.perf_counter() - t0
+    venv.close()
+    return {"envs": n, "stack_k": 10, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+            "env_steps_per_s": round(n * steps / el, 1),
+            "note": "numpy obs/rew/dones + N info dicts per step (SB3 VecEnv contract), device actions"}
+
+
 def load_traffic(envs, stack, state_bytes):
     """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if it was
     measured on this workload and state layout."""
@@ -276,6 +301,7 @@ def main():
     venv.close()
     del acts, warm
     torch.cuda.empty_cache()
+    sb3 = sb3_compat_bench(dev, n) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
         rollout = rollout_bench(args, dev, rank, world)
@@ -338,6 +364,8 @@ def main():
     }
     if rollout is not None:
         out["rollout"] = rollout
+    if sb3 is not None:
+        out["sb3_compat"] = sb3
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
     print(json.dumps(out), flush=True)

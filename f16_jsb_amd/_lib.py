@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-from .abi import EnvConfig
+from .abi import EnvConfig, RolloutSlot
 
 LIB_PATH = os.environ.get("F16ENV_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libf16env.so")
 
@@ -43,6 +43,7 @@ def lib():
     L.f16env_state_bytes_per_env.restype = i32
     L.f16env_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.f16env_step.argtypes = [vp] * 13
+    L.f16env_step_rollout.argtypes = [vp, vp, ctypes.POINTER(RolloutSlot)] + [vp] * 11
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
@@ -59,7 +60,7 @@ def lib():
     L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
     L.f16env_last_error.restype = ctypes.c_char_p
     for name in ("f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_reset",
-                 "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
+                 "f16env_step", "f16env_step_rollout", "f16env_get_state", "f16env_set_state", "f16env_trim",
                  "f16env_sample_actions", "f16env_gae", "f16env_features"):
         getattr(L, name).restype = i32
     _lib = L
@@ -75,7 +76,7 @@ def check(status: int, what: str):
 # symbols include/f16env.h declares (tests check the .so exports every one of them)
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
-    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_get_state",
+    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
 )

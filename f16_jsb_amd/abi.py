@@ -126,3 +126,16 @@ def config_cfg5(c: EnvConfig) -> EnvConfig:
 def algorithmic_bytes_per_env_step(stack_k: int, state_bytes: int) -> int:
     """B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S."""
     return 16 + 60 * stack_k + 60 * (stack_k - 1) + 4 + 2 + 2 * state_bytes
+
+
+class RolloutSlot(ctypes.Structure):
+    """f16env_rollout_slot (include/f16env.h): one slot of a device rollout buffer filled by
+    f16env_step_rollout; NULL pointers are not written."""
+    _fields_ = [
+        ("act_seed", ctypes.c_uint64),
+        ("act_step", ctypes.c_uint64),
+        ("frame", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p),
+        ("rewards", ctypes.c_void_p),
+        ("next_start", ctypes.c_void_p),
+    ]

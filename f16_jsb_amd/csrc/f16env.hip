@@ -98,6 +98,24 @@ __device__ __forceinline__ void rng_normals(uint64_t seed, uint64_t gid, uint32_
   xi[2] = r2 * c4;
 }
 
+// uniform action over the Box [-1,-1,-1,0]..[1,1,1,1] (jsbsim_gym.py:143-148) keyed by
+// (seed; global env id, step): the f16env_sample_actions stream, also drawn in-kernel by the
+// rollout step
+__device__ __forceinline__ float4 philox_action(uint64_t seed, uint64_t gid, uint64_t step) {
+  uint32_t o[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step,
+         (uint32_t)(step >> 32), o);
+  const float lo[4] = {-1.f, -1.f, -1.f, 0.f}, hi[4] = {1.f, 1.f, 1.f, 1.f};
+  float4 v;
+  float* pv = &v.x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float u = (float)(o[j] >> 8) * (1.0f / 16777216.0f);
+    pv[j] = lo[j] + (hi[j] - lo[j]) * u;
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------------------------------
 // IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
 // ------------------------------------------------------------------------------------------
@@ -331,6 +349,13 @@ struct StepArgs {
   int32_t* done_idx;
   int32_t* n_done;
   int32_t lds_image;
+  // rollout slot (f16env_step_rollout; all NULL / 0 for f16env_step)
+  int32_t sample_act;          // act == NULL: draw the actions in-kernel (seed, step)
+  uint64_t act_seed, act_step;
+  float* r_frame;              // N x 15: newest frame of obs_prev
+  float* r_act;                // N x 4: the actions applied
+  float* r_rew;                // N: rewards
+  float* r_next_start;         // N: done as 0/1 float (episode_starts of the next slot)
   EnvArgs E;
   ModelConsts C;
 };
@@ -394,13 +419,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
                                           reinterpret_cast<float*>(sTmpl));
   if (live) {
     lane_load<GUST>(a.s, k, L);
-    av = reinterpret_cast<const float4*>(a.act)[k];
+    if (!a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && !defined(F16_DMA_FIRST)
   issue_stack_dma();
 #endif
+  if (a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   float rew_out = 0.0f;
@@ -473,6 +499,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     a.rew[k] = rew_out;
     a.term[k] = (uint8_t)(flags_out & 1);
     a.trunc[k] = (uint8_t)(flags_out >> 1);
+    if (a.r_rew) a.r_rew[k] = rew_out;
+    if (a.r_act) reinterpret_cast<float4*>(a.r_act)[k] = av;
+    if (a.r_next_start) a.r_next_start[k] = done ? 1.0f : 0.0f;
     if (done) {
       if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
       if (a.ep_len) a.ep_len[k] = L.step;
@@ -500,6 +529,33 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
 #else
   constexpr bool kSkipStack = false;
 #endif
+  // rollout slot frame = newest frame of obs_prev (what the policy acted on), for every lane
+  if (a.r_frame && rows > 0) {
+    if (image) {
+      __builtin_amdgcn_wave_barrier();
+      float* dst = a.r_frame + row0 * F16_OBS_DIM;
+      if (rows == 64) {  // 960 floats = 240 float4, 16-B aligned (row0 is a multiple of 64)
+        for (int q = lane; q < 64 * F16_OBS_DIM / 4; q += 64) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int j = 4 * q + i, r = j / F16_OBS_DIM, c = j - r * F16_OBS_DIM;
+            v[i] = img[r * KC + HC + c];
+          }
+          reinterpret_cast<float4*>(dst)[q] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      } else {
+        for (int j = lane; j < rows * F16_OBS_DIM; j += 64) {
+          const int r = j / F16_OBS_DIM, c = j - r * F16_OBS_DIM;
+          dst[j] = img[r * KC + HC + c];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else if (live) {
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) a.r_frame[k * F16_OBS_DIM + c] = a.obs_prev[k * KC + HC + c];
+    }
+  }
   if (kSkipStack) {
   } else if (image) {
     // 2) splice the new frame of row r into the image at row r+1's first frame, which the
@@ -867,18 +923,7 @@ __global__ __launch_bounds__(BLOCK) void f16_trim_kernel(int64_t n, const double
 __global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t seed, uint64_t step, float* act) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const uint64_t gid = (uint64_t)(id_base + k);
-  uint32_t o[4];
-  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step,
-         (uint32_t)(step >> 32), o);
-  const float lo[4] = {-1.f, -1.f, -1.f, 0.f}, hi[4] = {1.f, 1.f, 1.f, 1.f};
-  float4 v;
-  float* pv = &v.x;
-  for (int j = 0; j < 4; ++j) {
-    const float u = (float)(o[j] >> 8) * (1.0f / 16777216.0f);
-    pv[j] = lo[j] + (hi[j] - lo[j]) * u;
-  }
-  reinterpret_cast<float4*>(act)[k] = v;
+  reinterpret_cast<float4*>(act)[k] = philox_action(seed, (uint64_t)(id_base + k), step);
 }
 
 // GAE(lambda) over a [n_steps][n_envs] rollout, one lane per env, backward in time.
@@ -1212,18 +1257,26 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   return 0;
 }
 
-int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_prev, float* obs, float* rew,
-                uint8_t* terminated, uint8_t* truncated, float* terminal_obs, double* ep_return, int32_t* ep_len,
-                int32_t* done_idx, int32_t* n_done) {
+static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                     const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
+                     float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done) {
   if (!h) return set_err(-1, "null handle");
-  if (!act || !obs_prev || !obs || !rew || !terminated || !truncated)
-    return set_err(-1, "act/obs_prev/obs/rew/terminated/truncated are required");
+  if ((!act && !slot) || !obs_prev || !obs || !rew || !terminated || !truncated)
+    return set_err(-1, "act (or a rollout slot)/obs_prev/obs/rew/terminated/truncated are required");
   if (done_idx && !n_done) return set_err(-1, "done_idx requires n_done");
-  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  if (act && ((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
   StepArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.act = act; a.obs_prev = obs_prev; a.obs = obs; a.rew = rew;
   a.term = terminated; a.trunc = truncated; a.tobs = terminal_obs; a.ep_ret = ep_return; a.ep_len = ep_len;
   a.done_idx = done_idx; a.n_done = n_done;
+  a.sample_act = act ? 0 : 1;
+  a.act_seed = slot ? slot->act_seed : 0; a.act_step = slot ? slot->act_step : 0;
+  a.r_frame = slot ? slot->frame : nullptr;
+  a.r_act = slot ? slot->actions : nullptr;
+  a.r_rew = slot ? slot->rewards : nullptr;
+  a.r_next_start = slot ? slot->next_start : nullptr;
+  if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
+    return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = h->lds_image;
@@ -1247,6 +1300,22 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
     HIPCHK(hipGetLastError());
   }
   return 0;
+}
+
+int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_prev, float* obs, float* rew,
+                uint8_t* terminated, uint8_t* truncated, float* terminal_obs, double* ep_return, int32_t* ep_len,
+                int32_t* done_idx, int32_t* n_done) {
+  return step_impl(h, stream, nullptr, act, obs_prev, obs, rew, terminated, truncated, terminal_obs, ep_return,
+                   ep_len, done_idx, n_done);
+}
+
+int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                        const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
+                        float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx,
+                        int32_t* n_done) {
+  if (!slot) return set_err(-1, "null rollout slot");
+  return step_impl(h, stream, slot, act, obs_prev, obs, rew, terminated, truncated, terminal_obs, ep_return,
+                   ep_len, done_idx, n_done);
 }
 
 int f16env_get_state(f16env_t h, void* stream, double* canon) {

@@ -21,7 +21,7 @@ import numpy as np
 
 from . import spaces
 from ._lib import F16EnvError, check, lib
-from .abi import (F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC,
+from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
 StepOut = namedtuple("StepOut", "obs rew terminated truncated terminal_obs ep_return ep_len")
@@ -156,6 +156,27 @@ class F16Envs:
         check(lib().f16env_step(self._h, self._stream(), _ptr(act), _ptr(prev), _ptr(nxt), _ptr(self.rew),
                                 _ptr(self.term), _ptr(self.trunc), _ptr(self.terminal_obs),
                                 _ptr(self.ep_return), _ptr(self.ep_len), _ptr(done_idx), _ptr(n_done)), "f16env_step")
+        self._cur ^= 1
+        return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
+
+    def step_rollout(self, seed: int, step: int, frame=None, actions=None, rewards=None, next_start=None,
+                     policy_actions=None) -> StepOut:
+        """One env step that also writes one rollout-buffer slot (f16env_step_rollout): the
+        newest frame of the observation acted on, the actions, the rewards and the next slot's
+        episode starts, with no extra launch. policy_actions None: actions drawn in-kernel
+        from the sample_actions(seed, step) stream (bit-identical)."""
+        t = self.torch
+        act = None
+        if policy_actions is not None:
+            self._act.copy_(t.as_tensor(policy_actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
+            act = self._act
+        slot = RolloutSlot(int(seed) & 0xFFFFFFFFFFFFFFFF, int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(frame),
+                           _ptr(actions), _ptr(rewards), _ptr(next_start))
+        prev = self._obs[self._cur]
+        nxt = self._obs[self._cur ^ 1]
+        check(lib().f16env_step_rollout(self._h, self._stream(), ctypes.byref(slot), _ptr(act), _ptr(prev), _ptr(nxt),
+                                        _ptr(self.rew), _ptr(self.term), _ptr(self.trunc), _ptr(self.terminal_obs),
+                                        _ptr(self.ep_return), _ptr(self.ep_len), None, None), "f16env_step_rollout")
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 

@@ -87,11 +87,15 @@ class DeviceRolloutBuffer:
         return {f: getattr(self, f) for f in FIELDS} | {"obs0": self.obs0}
 
 
-def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None):
+def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None, fused: bool = True):
     """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors with random
     policy actions from the device Philox stream (the policy network is out of scope; values
     and log-probs are zeros unless ``values_fn(obs) -> (values, log_probs)`` is given).
-    Starts from envs' current observation; returns (last_values, last_dones) for GAE."""
+    Starts from envs' current observation; returns (last_values, last_dones) for GAE.
+
+    fused: each step is ONE launch (f16env_step_rollout) that draws the actions in-kernel and
+    writes the slot's frame / actions / rewards / next episode starts itself, instead of a
+    sampling launch, the step and six buffer copies (RolloutBuffer.add, buffers.py:440-479)."""
     dev = buf.device
     n = buf.n_envs
     zeros = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -100,17 +104,39 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, v
     if starts is None:
         starts = torch.ones(n, dtype=torch.float32, device=dev)
     buf.reset()
-    for t in range(buf.n_steps):
-        act = envs.sample_actions(seed, step0 + t)
-        v, lp = values_fn(obs) if values_fn is not None else (zeros, zeros)
-        out = envs.step(act)
-        rew = out.rew
-        if values_fn is not None:
-            tv, _ = values_fn(out.terminal_obs)
-            rew = bootstrap_timeouts(rew, out.terminated, out.truncated, tv, buf.gamma)
-        buf.add(obs, act, rew, starts, v, lp)
-        obs = out.obs
-        starts = (out.terminated | out.truncated).to(torch.float32)
+    use_fused = fused and hasattr(envs, "step_rollout") and buf.frames[0].data_ptr() % 16 == 0 \
+        and (n * F16_OBS_DIM * 4) % 16 == 0
+    if use_fused:
+        carry = torch.empty(n, dtype=torch.float32, device=dev)
+        buf.obs0.copy_(obs)
+        buf.episode_starts[0].copy_(starts)
+        T = buf.n_steps
+        for t in range(T):
+            if values_fn is not None:
+                v, lp = values_fn(obs)
+                buf.values[t].copy_(v.reshape(-1))
+                buf.log_probs[t].copy_(lp.reshape(-1))
+            nxt = buf.episode_starts[t + 1] if t + 1 < T else carry
+            out = envs.step_rollout(seed, step0 + t, frame=buf.frames[t], actions=buf.actions[t],
+                                    rewards=buf.rewards[t], next_start=nxt)
+            if values_fn is not None:
+                tv, _ = values_fn(out.terminal_obs)
+                buf.rewards[t].copy_(bootstrap_timeouts(buf.rewards[t], out.terminated, out.truncated, tv, buf.gamma))
+            obs = out.obs
+        buf.pos = T
+        starts = carry
+    else:
+        for t in range(buf.n_steps):
+            act = envs.sample_actions(seed, step0 + t)
+            v, lp = values_fn(obs) if values_fn is not None else (zeros, zeros)
+            out = envs.step(act)
+            rew = out.rew
+            if values_fn is not None:
+                tv, _ = values_fn(out.terminal_obs)
+                rew = bootstrap_timeouts(rew, out.terminated, out.truncated, tv, buf.gamma)
+            buf.add(obs, act, rew, starts, v, lp)
+            obs = out.obs
+            starts = (out.terminated | out.truncated).to(torch.float32)
     envs._last_episode_starts = starts
     last_v = values_fn(obs)[0] if values_fn is not None else zeros
     return last_v, starts

@@ -21,6 +21,7 @@
  *                      parity replay and checkpoint/restore)
  *   f16env_trim     <- no reference equivalent (the reference never trims; BASELINE cfg 2)
  *   f16env_sample_actions <- action_space.sample() (jsbsim_gym.py:575), device Philox
+ *   f16env_step_rollout <- f16env_step + buffers.py:440-479 RolloutBuffer.add (8f rank 1)
  *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
  *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
  */
@@ -184,6 +185,29 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
 int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_prev, float* obs,
                 float* rew, uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
                 double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done);
+
+/* One env step that also fills one slot of a device rollout buffer (SURVEY.md 8f rank 1,
+ * replacing the per-step stable_baselines3 RolloutBuffer.add, buffers.py:440-479, and the
+ * action sampling of collect_rollouts, on_policy_algorithm.py:194-218, with no extra launch).
+ * Every pointer of the slot may be NULL (not written):
+ *   frame      N x 15 float: newest frame of obs_prev, i.e. of the observation acted on
+ *              (frame-deduplicated storage; f16_jsb_amd/rollout.py rebuilds stacks)
+ *   actions    N x 4 float: the actions applied
+ *   rewards    N float: the step's rewards (same values as rew)
+ *   next_start N float: 1.0 where the lane finished (episode_starts of the NEXT slot), else 0
+ * act == NULL draws the actions in-kernel from the f16env_sample_actions stream
+ * (act_seed, act_step), bit-identical to f16env_sample_actions followed by f16env_step. */
+typedef struct f16env_rollout_slot {
+  uint64_t act_seed, act_step;
+  float* frame;
+  float* actions;
+  float* rewards;
+  float* next_start;
+} f16env_rollout_slot;
+int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                        const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
+                        float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx,
+                        int32_t* n_done);
 
 /* Canonical state export/import: canon is N x F16C_N double (device). */
 int f16env_get_state(f16env_t h, void* stream, double* canon);

@@ -94,3 +94,39 @@ def test_two_wave_variant_matches_one_wave_variant(gpu, monkeypatch):
     torch.testing.assert_close(outs[1][0], outs[0][0], rtol=0, atol=0)
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=0, atol=0)
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("n,k", [(4096, 4), (1000, 10), (777, 3)])
+def test_fused_rollout_step_equals_sample_step_add(gpu, n, k):
+    """f16env_step_rollout (one launch: in-kernel Philox actions + the slot's frame / actions /
+    rewards / next episode starts) fills the buffer bit-identically to the unfused
+    sample_actions -> step -> RolloutBuffer.add sequence, and leaves the envs in the same
+    state; crashing lanes exercise the done-row paths, ragged N the partial last wave."""
+    import torch
+    from oracle_ref import default_ic
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout
+    T = 48
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(150.0, 9000.0, n)
+    ic[:, 7] = -0.35
+    bufs, envs = [], []
+    for fused in (False, True):
+        e = F16Envs(n, stack_k=k, seed=4)
+        e.reset(ic=ic)
+        b = DeviceRolloutBuffer(T, n, k, gpu)
+        collect_rollout(e, DeviceRolloutBuffer(3, n, k, gpu), 17, fused=fused)  # carry-over starts
+        last_v, last_d = collect_rollout(e, b, 21, step0=100, fused=fused)
+        bufs.append((b, last_d.clone()))
+        envs.append(e)
+    (b0, d0), (b1, d1) = bufs
+    assert int(b0.episode_starts[1:].sum().item()) > 0, "expected auto-resets in the rollout"
+    for f in ("frames", "actions", "rewards", "episode_starts", "obs0"):
+        assert torch.equal(getattr(b0, f), getattr(b1, f)), f
+    assert torch.equal(d0, d1)
+    assert torch.equal(envs[0].obs, envs[1].obs)
+    assert torch.equal(envs[0].get_state(), envs[1].get_state())
+    # the rebuilt stacks are the env's observations
+    assert torch.equal(b1.observations(steps=[T - 1])[0], b1.observations()[T - 1])
+    for e in envs:
+        e.close()
