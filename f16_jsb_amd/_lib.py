@@ -21,6 +21,14 @@ class F16EnvError(RuntimeError):
     pass
 
 
+def _set(L, name, argtypes, restype):
+    """Declare an entry point; tolerate its absence in an older build (tools/variant_sweep.py
+    times earlier libraries side by side -- tests check the product exports every symbol)."""
+    f = getattr(L, name, None)
+    if f is not None:
+        f.argtypes, f.restype = argtypes, restype
+
+
 def lib():
     """Load libf16env.so (raises F16EnvError if it was not built)."""
     global _lib
@@ -43,7 +51,7 @@ def lib():
     L.f16env_state_bytes_per_env.restype = i32
     L.f16env_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.f16env_step.argtypes = [vp] * 13
-    L.f16env_step_rollout.argtypes = [vp, vp, ctypes.POINTER(RolloutSlot)] + [vp] * 11
+    _set(L, "f16env_step_rollout", [vp, vp, ctypes.POINTER(RolloutSlot)] + [vp] * 11, i32)
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
@@ -54,13 +62,12 @@ def lib():
     L.f16env_step_kernel_name.restype = ctypes.c_char_p
     L.f16env_step_waves_per_simd.argtypes = [vp]
     L.f16env_step_waves_per_simd.restype = i32
-    L.f16env_step_variant.argtypes = [vp]
-    L.f16env_step_variant.restype = i32
+    _set(L, "f16env_step_variant", [vp], i32)
     L.f16env_algorithmic_bytes_per_env_step.argtypes = [i32]
     L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
     L.f16env_last_error.restype = ctypes.c_char_p
     for name in ("f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_reset",
-                 "f16env_step", "f16env_step_rollout", "f16env_get_state", "f16env_set_state", "f16env_trim",
+                 "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
                  "f16env_sample_actions", "f16env_gae", "f16env_features"):
         getattr(L, name).restype = i32
     _lib = L

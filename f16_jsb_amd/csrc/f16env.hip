@@ -375,7 +375,7 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
 // frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
 // 160 KB). sT is then unused.
-template <int MODE, bool GT = false>
+template <int MODE, bool GT = false, bool ROLL = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
@@ -419,14 +419,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
                                           reinterpret_cast<float*>(sTmpl));
   if (live) {
     lane_load<GUST>(a.s, k, L);
-    if (!a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
+    if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && !defined(F16_DMA_FIRST)
   issue_stack_dma();
 #endif
-  if (a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
+  if (ROLL && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   float rew_out = 0.0f;
@@ -499,9 +499,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     a.rew[k] = rew_out;
     a.term[k] = (uint8_t)(flags_out & 1);
     a.trunc[k] = (uint8_t)(flags_out >> 1);
-    if (a.r_rew) a.r_rew[k] = rew_out;
-    if (a.r_act) reinterpret_cast<float4*>(a.r_act)[k] = av;
-    if (a.r_next_start) a.r_next_start[k] = done ? 1.0f : 0.0f;
+    if (ROLL) {
+      if (a.r_rew) a.r_rew[k] = rew_out;
+      if (a.r_act) reinterpret_cast<float4*>(a.r_act)[k] = av;
+      if (a.r_next_start) a.r_next_start[k] = done ? 1.0f : 0.0f;
+    }
     if (done) {
       if (a.ep_ret) a.ep_ret[k] = L.ep_ret;
       if (a.ep_len) a.ep_len[k] = L.step;
@@ -530,7 +532,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   constexpr bool kSkipStack = false;
 #endif
   // rollout slot frame = newest frame of obs_prev (what the policy acted on), for every lane
-  if (a.r_frame && rows > 0) {
+  if (ROLL && a.r_frame && rows > 0) {
     if (image) {
       __builtin_amdgcn_wave_barrier();
       float* dst = a.r_frame + row0 * F16_OBS_DIM;
@@ -678,27 +680,34 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(StepArgs a) {
   STEP_SHARED
   step_body<0>(a, sT, sTmpl, sDone, dynl);
 }
-template <int MODE, int OCC>
+template <int MODE, int OCC, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
   STEP_SHARED
-  step_body<MODE>(a, sT, sTmpl, sDone, dynl);
+  step_body<MODE, false, ROLL>(a, sT, sTmpl, sDone, dynl);
 }
 // global-table variant (large K on the LDS-image path): no LDS table copy
-template <int MODE>
+template <int MODE, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
   __shared__ __align__(16) float4 sTmpl[NCOL];
   __shared__ int sDone[BLOCK];
   extern __shared__ __align__(16) float dynl[];
-  step_body<MODE, true>(a, nullptr, sTmpl, sDone, dynl);
+  step_body<MODE, true, ROLL>(a, nullptr, sTmpl, sDone, dynl);
 }
 using StepKernel = void (*)(StepArgs);
-// variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables
-static StepKernel step_kernel_for(int mode, int variant) {
-  static const StepKernel table[3][4] = {
-      {f16_step_kernel, f16_step_var_kernel<1, 1>, f16_step_var_kernel<2, 1>, f16_step_var_kernel<3, 1>},
-      {f16_step_var_kernel<0, 2>, f16_step_var_kernel<1, 2>, f16_step_var_kernel<2, 2>, f16_step_var_kernel<3, 2>},
-      {f16_step_gt_kernel<0>, f16_step_gt_kernel<1>, f16_step_gt_kernel<2>, f16_step_gt_kernel<3>}};
-  return table[variant < 0 || variant > 2 ? 0 : variant][mode & 3];
+// variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
+// roll: the rollout-slot build (f16env_step_rollout); the plain step carries none of its code.
+static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {
+  static const StepKernel table[2][3][4] = {
+      {{f16_step_kernel, f16_step_var_kernel<1, 1>, f16_step_var_kernel<2, 1>, f16_step_var_kernel<3, 1>},
+       {f16_step_var_kernel<0, 2>, f16_step_var_kernel<1, 2>, f16_step_var_kernel<2, 2>, f16_step_var_kernel<3, 2>},
+       {f16_step_gt_kernel<0>, f16_step_gt_kernel<1>, f16_step_gt_kernel<2>, f16_step_gt_kernel<3>}},
+      {{f16_step_var_kernel<0, 1, true>, f16_step_var_kernel<1, 1, true>, f16_step_var_kernel<2, 1, true>,
+        f16_step_var_kernel<3, 1, true>},
+       {f16_step_var_kernel<0, 2, true>, f16_step_var_kernel<1, 2, true>, f16_step_var_kernel<2, 2, true>,
+        f16_step_var_kernel<3, 2, true>},
+       {f16_step_gt_kernel<0, true>, f16_step_gt_kernel<1, true>, f16_step_gt_kernel<2, true>,
+        f16_step_gt_kernel<3, true>}}};
+  return table[roll ? 1 : 0][variant < 0 || variant > 2 ? 0 : variant][mode & 3];
 }
 
 // cfg5 auto-reset of the lanes a deferred-mode step finished (done list from its ballot
@@ -1199,8 +1208,8 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     h->dyn_lds = h->lds_image ? img : fallback;
     for (int v = 0; v <= 2; ++v) {
       if ((v == 2 ? static_gt : static_lds) + h->dyn_lds > 160 * 1024) continue;  // not launchable here
-      for (int m = 0; m < 4; ++m)
-        if (hipFuncSetAttribute((const void*)step_kernel_for(m, v), hipFuncAttributeMaxDynamicSharedMemorySize,
+      for (int m = 0; m < 8; ++m)
+        if (hipFuncSetAttribute((const void*)step_kernel_for(m & 3, v, m >= 4), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)h->dyn_lds) != hipSuccess) {
           (void)hipGetLastError();
           hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
@@ -1289,7 +1298,8 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   }
   if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  hipLaunchKernelGGL(step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0)), grid, blk, h->dyn_lds, st, a);
+  hipLaunchKernelGGL(step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0), slot != nullptr), grid, blk,
+                     h->dyn_lds, st, a);
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
