@@ -59,6 +59,7 @@ def lib():
     L.f16env_gae.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, ctypes.c_double,
                              ctypes.c_double, vp, vp]
     L.f16env_features.argtypes = [vp, ctypes.c_int64, vp, vp]
+    _set(L, "f16env_poses", [vp, ctypes.c_int64, vp, ctypes.c_int64, vp], i32)
     L.f16env_step_kernel_name.restype = ctypes.c_char_p
     L.f16env_step_waves_per_simd.argtypes = [vp]
     L.f16env_step_waves_per_simd.restype = i32
@@ -84,6 +85,6 @@ def check(status: int, what: str):
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_get_state",
-    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant",
+    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
 )

@@ -1024,6 +1024,41 @@ __global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, con
   }
 }
 
+// Render/telemetry poses of one frame per env: what JSBSimEnv.render
+// (jsbsim_gym/jsbsim_gym.py:381-415) hands the Viewer -- the aircraft position in viewer axes
+// (-y, h, x) * 1e-3, its attitude Quaternion.from_euler(phi, theta, psi) (visualization/
+// quaternion.py:38-45, q_psi * q_theta * q_phi) remapped (w, -y, -z, x), and the goal position
+// in viewer axes -- in float32 with the reference's operation order. One lane per env; frames
+// are read with a caller stride so obs[:, -1, :] of a (N, K, 15) stack needs no copy.
+__device__ __forceinline__ void quat_mul_ref(const float* a, const float* b, float* o) {
+#pragma clang fp contract(off)
+  // quaternion.py:11-14: w = a0 b0 - a.b ; v = a0 b + b0 a + a x b  (float32, left to right)
+  const float dot = a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+  o[0] = a[0] * b[0] - dot;
+  const float cx = a[2] * b[3] - a[3] * b[2], cy = a[3] * b[1] - a[1] * b[3], cz = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[0] * b[1] + b[0] * a[1] + cx;
+  o[2] = a[0] * b[2] + b[0] * a[2] + cy;
+  o[3] = a[0] * b[3] + b[0] * a[3] + cz;
+}
+__global__ void f16_poses_kernel(int64_t n, const float* __restrict__ frames, int64_t stride, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float* f = frames + k * stride;
+  const float s = 1e-3f;
+  float* o = out + k * 10;
+  o[0] = -f[1] * s; o[1] = f[2] * s; o[2] = f[0] * s;
+  const float hp = f[9] / 2.0f, ht = f[10] / 2.0f, hs = f[11] / 2.0f;
+  const float q1[4] = {cosf(hp), sinf(hp), 0.0f, 0.0f};
+  const float q2[4] = {cosf(ht), 0.0f, sinf(ht), 0.0f};
+  const float q3[4] = {cosf(hs), 0.0f, 0.0f, sinf(hs)};
+  float q32[4], q[4];
+  quat_mul_ref(q3, q2, q32);
+  quat_mul_ref(q32, q1, q);
+  o[3] = q[0]; o[4] = -q[2]; o[5] = -q[3]; o[6] = q[1];
+  o[7] = -f[13] * s; o[8] = f[14] * s; o[9] = f[12] * s;
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -1381,6 +1416,16 @@ int f16env_features(void* stream, int64_t n_frames, const float* obs, float* fea
   if (blocks > 0x7fffffffLL) return set_err(-1, "n_frames too large");
   hipLaunchKernelGGL(f16_features_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_frames, obs,
                      feat);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_poses(void* stream, int64_t n, const float* frames, int64_t frame_stride, float* out) {
+  if (n < 0 || frame_stride < F16_OBS_DIM) return set_err(-1, "n >= 0 and frame_stride >= 15 required");
+  if (n == 0) return 0;
+  if (!frames || !out) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_poses_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, frames,
+                     frame_stride, out);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -24,6 +24,7 @@
  *   f16env_step_rollout <- f16env_step + buffers.py:440-479 RolloutBuffer.add (8f rank 1)
  *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
  *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
+ *   f16env_poses    <- jsbsim_gym.py:381-415 JSBSimEnv.render state -> Viewer poses (8f rank 4)
  */
 #ifndef F16ENV_H
 #define F16ENV_H
@@ -240,6 +241,15 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
  *        with d = |goal - pos|_xy, dz = goal_z - h, rb = atan2(dy, dx) - psi.
  * No handle needed; stream-ordered. */
 int f16env_features(void* stream, int64_t n_frames, const float* obs, float* feat);
+
+/* Render/telemetry poses, replacing the state -> Viewer transform of
+ * jsbsim_gym.py:381-415 (JSBSimEnv.render) for every env at once, float32:
+ *   frames  n frames of 15 floats, frame i at frames + i * frame_stride (e.g. the newest frame
+ *           of an N x K x 15 stack: frames = obs + 15 (K-1), frame_stride = 15 K)
+ *   out     n x 10 float: aircraft position in viewer axes (-y, h, x) * 1e-3, attitude
+ *           quaternion Quaternion.from_euler(phi, theta, psi) remapped to (w, -y, -z, x), goal
+ *           position in viewer axes (-gy, gz, gx) * 1e-3. */
+int f16env_poses(void* stream, int64_t n, const float* frames, int64_t frame_stride, float* out);
 
 /* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
  * HBM bytes one env-step moves. */
