@@ -179,9 +179,25 @@ def features_bench(envs, stream, iters=200):
     ms = s.elapsed_time(e) / iters
     frames = obs.numel() // 15
     gbps = frames * (15 + 17) * 4 / (ms * 1e-3) / 1e9
+    # the same features emitted alongside obs by the step call (F16Envs.step(..., features=)):
+    # marginal cost per step vs a plain step, same actions
+    n = obs.shape[0]
+    act = envs.sample_actions(99, 0)
+    for _ in range(5):
+        envs.step(act, features=out)
+    t = []
+    for use in (False, True, False, True):
+        s.record(stream)
+        for _ in range(iters // 2):
+            envs.step(act, features=out if use else None)
+        e.record(stream)
+        torch.cuda.synchronize()
+        t.append(s.elapsed_time(e) / (iters // 2))
+    plain, fused = min(t[0], t[2]), min(t[1], t[3])
     return {"kernel": "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
             "frames_per_s": round(frames / (ms * 1e-3), 1), "achieved_GBps": round(gbps, 1),
-            "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128}
+            "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128,
+            "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5)}
 
 
 def sb3_compat_bench(dev, n, steps=20):

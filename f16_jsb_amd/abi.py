@@ -138,4 +138,5 @@ class RolloutSlot(ctypes.Structure):
         ("actions", ctypes.c_void_p),
         ("rewards", ctypes.c_void_p),
         ("next_start", ctypes.c_void_p),
+        ("features", ctypes.c_void_p),
     ]

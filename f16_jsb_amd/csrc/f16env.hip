@@ -116,6 +116,31 @@ __device__ __forceinline__ float4 philox_action(uint64_t seed, uint64_t gid, uin
   return v;
 }
 
+#define FEAT_IN 15
+#define FEAT_OUT 17
+// jsbsim_gym/features.py:37-67 on one frame o[15] -> y[17], float32 with torch's per-op
+// rounding (IEEE division / sqrt, no FMA contraction, ~1-ulp atan2 / cos / sin)
+__device__ __forceinline__ void frame_features(const float* o, float* y) {
+#pragma clang fp contract(off)
+  // features.py:39-45 unpack; :47-53 position transform
+  const float dx = o[12] - o[0], dy = o[13] - o[1], dz = o[14] - o[2];
+  float d2 = dx * dx;
+  d2 = __fadd_rn(d2, __fmul_rn(dy, dy));
+  const float distance = __fsqrt_rn(d2);
+  const float abs_bearing = atan2f(dy, dx);
+  const float rel_bearing = abs_bearing - o[11];
+  y[0] = __fdiv_rn(1.0f, __fadd_rn(1.0f, __fmul_rn(distance, 1e-3f)));  // :56 dist_norm
+  y[1] = __fdiv_rn(dz, 15000.0f);                                         // :59 dz_norm
+  y[2] = __fdiv_rn(o[2], 15000.0f);                                       // :60 alt_norm
+  y[3] = o[3];                                                            // mach
+  y[4] = o[6]; y[5] = o[7]; y[6] = o[8];                                  // angular rates
+  y[7] = cosf(o[4]); y[8] = cosf(o[5]);                                   // :63 cos(alpha, beta)
+  y[9] = sinf(o[4]); y[10] = sinf(o[5]);                                  //     sin(alpha, beta)
+  y[11] = cosf(o[9]); y[12] = cosf(o[10]);                                // :64 cos(phi, theta)
+  y[13] = sinf(o[9]); y[14] = sinf(o[10]);                                //     sin(phi, theta)
+  y[15] = cosf(rel_bearing); y[16] = sinf(rel_bearing);                   // :65
+}
+
 // ------------------------------------------------------------------------------------------
 // IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
 // ------------------------------------------------------------------------------------------
@@ -971,8 +996,6 @@ __global__ void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __r
 // LMA_features.py:744-776 StackedLMAFeaturesExtractor does. HBM-bound (60 B in, 68 B out per
 // frame): each 256-thread block moves its 256 frames as coalesced float4 through LDS (frame
 // strides 15 and 17 are odd, so the per-thread LDS reads/writes are bank-conflict free).
-#define FEAT_IN 15
-#define FEAT_OUT 17
 __global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, const float* __restrict__ obs,
                                                            float* __restrict__ feat) {
   __shared__ __align__(16) float sIn[256 * FEAT_IN];
@@ -993,28 +1016,7 @@ __global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, con
     for (int q = t; q < nf * FEAT_IN; q += 256) sIn[q] = gin[q];
   }
   __syncthreads();
-  if (t < nf) {
-#pragma clang fp contract(off)  // torch float32: every product and sum rounded separately
-    const float* o = sIn + t * FEAT_IN;
-    float* y = sOut + t * FEAT_OUT;
-    // features.py:39-45 unpack; :47-53 position transform
-    const float dx = o[12] - o[0], dy = o[13] - o[1], dz = o[14] - o[2];
-    float d2 = dx * dx;
-    d2 = __fadd_rn(d2, __fmul_rn(dy, dy));
-    const float distance = __fsqrt_rn(d2);
-    const float abs_bearing = atan2f(dy, dx);
-    const float rel_bearing = abs_bearing - o[11];
-    y[0] = __fdiv_rn(1.0f, __fadd_rn(1.0f, __fmul_rn(distance, 1e-3f)));  // :56 dist_norm
-    y[1] = __fdiv_rn(dz, 15000.0f);                                         // :59 dz_norm
-    y[2] = __fdiv_rn(o[2], 15000.0f);                                       // :60 alt_norm
-    y[3] = o[3];                                                            // mach
-    y[4] = o[6]; y[5] = o[7]; y[6] = o[8];                                  // angular rates
-    y[7] = cosf(o[4]); y[8] = cosf(o[5]);                                   // :63 cos(alpha, beta)
-    y[9] = sinf(o[4]); y[10] = sinf(o[5]);                                  //     sin(alpha, beta)
-    y[11] = cosf(o[9]); y[12] = cosf(o[10]);                                // :64 cos(phi, theta)
-    y[13] = sinf(o[9]); y[14] = sinf(o[10]);                                //     sin(phi, theta)
-    y[15] = cosf(rel_bearing); y[16] = sinf(rel_bearing);                   // :65
-  }
+  if (t < nf) frame_features(sIn + t * FEAT_IN, sOut + t * FEAT_OUT);
   __syncthreads();
   if (vout) {
     for (int q = t; q < 256 * FEAT_OUT / 4; q += 256)
@@ -1241,16 +1243,6 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     h->gt = (h->lds_image && img + static_lds > 160 * 1024) ? 1 : 0;
     if (getenv("F16ENV_GT") && h->lds_image) h->gt = atoi(getenv("F16ENV_GT")) ? 1 : 0;
     h->dyn_lds = h->lds_image ? img : fallback;
-    for (int v = 0; v <= 2; ++v) {
-      if ((v == 2 ? static_gt : static_lds) + h->dyn_lds > 160 * 1024) continue;  // not launchable here
-      for (int m = 0; m < 8; ++m)
-        if (hipFuncSetAttribute((const void*)step_kernel_for(m & 3, v, m >= 4), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)h->dyn_lds) != hipSuccess) {
-          (void)hipGetLastError();
-          hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
-          return set_err(-2, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-        }
-    }
     // two waves per SIMD only pay when there are more waves than SIMDs and two workgroups'
     // LDS (tables + stack image) fit in one CU
     int cus = 0;
@@ -1259,6 +1251,19 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const int64_t waves = ((int64_t)cfg->n_envs + 63) / 64;
     h->occ = (!h->gt && waves > 4 * (int64_t)cus && 2 * (static_lds + h->dyn_lds) <= 160 * 1024) ? 2 : 1;
     if (getenv("F16ENV_OCC")) h->occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
+    for (int v = 0; v <= 2; ++v) {
+      const size_t st_v = v == 2 ? static_gt : static_lds;
+      for (int m = 0; m < 8; ++m) {
+        const size_t dyn = h->dyn_lds;
+        if (st_v + dyn > 160 * 1024) continue;  // not launchable in this configuration
+        if (hipFuncSetAttribute((const void*)step_kernel_for(m & 3, v, m >= 4), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dyn) != hipSuccess) {
+          (void)hipGetLastError();
+          hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
+          return set_err(-2, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        }
+      }
+    }
   }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + F16_IC_N, cfg->ic_lo, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
@@ -1319,6 +1324,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   a.r_act = slot ? slot->actions : nullptr;
   a.r_rew = slot ? slot->rewards : nullptr;
   a.r_next_start = slot ? slot->next_start : nullptr;
+  float* feat = slot ? slot->features : nullptr;
   if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
     return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
   a.E = env_args(h);
@@ -1342,6 +1348,12 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
+    HIPCHK(hipGetLastError());
+  }
+  if (feat) {  // policy features of the returned obs (after any deferred reset rewrote rows)
+    const int64_t nf = (int64_t)a.E.n * a.E.K;
+    hipLaunchKernelGGL(f16_features_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, nf,
+                       (const float*)obs, feat);
     HIPCHK(hipGetLastError());
   }
   return 0;

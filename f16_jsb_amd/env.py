@@ -137,11 +137,14 @@ class F16Envs:
         check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
         return out
 
-    def step(self, actions, done_idx=None, n_done=None) -> StepOut:
+    def step(self, actions, done_idx=None, n_done=None, features=None) -> StepOut:
         """One env step for all lanes; ``actions`` (N,4) float32 device tensor (or host
         array, copied). Returns device tensors; obs alternates between two buffers.
         done_idx (N,) / n_done (1,) int32 device tensors receive the compacted list of lanes
-        that finished (optional)."""
+        that finished (optional). features: an (N, K, 17) float32 device tensor that receives
+        the policy features of the returned obs (features.py:37-67) in the same call."""
+        if features is not None:
+            return self.step_rollout(0, 0, features=features, policy_actions=actions)
         t = self.torch
         if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
                 and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
@@ -160,7 +163,7 @@ class F16Envs:
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
     def step_rollout(self, seed: int, step: int, frame=None, actions=None, rewards=None, next_start=None,
-                     policy_actions=None) -> StepOut:
+                     policy_actions=None, features=None) -> StepOut:
         """One env step that also writes one rollout-buffer slot (f16env_step_rollout): the
         newest frame of the observation acted on, the actions, the rewards and the next slot's
         episode starts, with no extra launch. policy_actions None: actions drawn in-kernel
@@ -168,10 +171,18 @@ class F16Envs:
         t = self.torch
         act = None
         if policy_actions is not None:
-            self._act.copy_(t.as_tensor(policy_actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
-            act = self._act
+            if isinstance(policy_actions, t.Tensor) and policy_actions.device == self.device \
+                    and policy_actions.dtype == t.float32 and policy_actions.is_contiguous() \
+                    and policy_actions.data_ptr() % 16 == 0:
+                act = policy_actions
+            else:
+                self._act.copy_(t.as_tensor(policy_actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
+                act = self._act
+        if features is not None and (tuple(features.shape) != (self.n, self.k, 17) or features.dtype != t.float32
+                                     or not features.is_contiguous()):
+            raise ValueError("features must be a contiguous float32 (N, K, 17) tensor")
         slot = RolloutSlot(int(seed) & 0xFFFFFFFFFFFFFFFF, int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(frame),
-                           _ptr(actions), _ptr(rewards), _ptr(next_start))
+                           _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(features))
         prev = self._obs[self._cur]
         nxt = self._obs[self._cur ^ 1]
         check(lib().f16env_step_rollout(self._h, self._stream(), ctypes.byref(slot), _ptr(act), _ptr(prev), _ptr(nxt),

@@ -196,6 +196,7 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
  *   actions    N x 4 float: the actions applied
  *   rewards    N float: the step's rewards (same values as rew)
  *   next_start N float: 1.0 where the lane finished (episode_starts of the NEXT slot), else 0
+ *   features   N x K x 17 float: policy features of the returned observation (below)
  * act == NULL draws the actions in-kernel from the f16env_sample_actions stream
  * (act_seed, act_step), bit-identical to f16env_sample_actions followed by f16env_step. */
 typedef struct f16env_rollout_slot {
@@ -204,6 +205,9 @@ typedef struct f16env_rollout_slot {
   float* actions;
   float* rewards;
   float* next_start;
+  float* features;  /* N x K x 17: policy features of the returned obs (features.py:37-67, as
+                       f16env_features), by a second launch in the same call (an epilogue
+                       fused into the step kernel measured slower: +9.5 vs +9 us) */
 } f16env_rollout_slot;
 int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                         const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,

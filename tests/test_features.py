@@ -121,3 +121,27 @@ def test_features_rejects_bad_input():
         features(torch.zeros(4, 14))
     with pytest.raises(TypeError):
         features(torch.zeros(4, 15))  # CPU tensor: the product path has no CPU fallback
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,cfg5", [(4096, 4, False), (1000, 4, False), (777, 8, False), (2048, 4, True)])
+def test_gpu_step_features_equal_separate_kernel(gpu, n, k, cfg5):
+    """F16Envs.step(..., features=f): the features of the returned obs computed in the same
+    call, bit-identical to f16env_features over the same obs -- including the rows of lanes
+    that finished and were reset during the step (cfg5: after the deferred-reset kernel)."""
+    from oracle_ref import default_ic
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.features import features
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(150.0, 9000.0, n)
+    ic[:, 7] = -0.35
+    e = F16Envs(n, stack_k=k, seed=6, cfg5=cfg5)
+    e.reset(ic=None if cfg5 else ic)
+    f = torch.empty((n, k, 17), dtype=torch.float32, device=gpu)
+    done_total = 0
+    for t in range(25):
+        out = e.step(e.sample_actions(8, t), features=f)
+        done_total += int((out.terminated | out.truncated).sum())
+        assert torch.equal(f, features(out.obs)), "step %d" % t
+    assert cfg5 or done_total > 0
+    e.close()
