@@ -64,6 +64,9 @@ def lib():
     L.f16env_step_waves_per_simd.argtypes = [vp]
     L.f16env_step_waves_per_simd.restype = i32
     _set(L, "f16env_step_variant", [vp], i32)
+    _set(L, "f16env_profile_begin", [vp, i32], i32)
+    _set(L, "f16env_profile_end", [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_int)], i32)
     L.f16env_algorithmic_bytes_per_env_step.argtypes = [i32]
     L.f16env_algorithmic_bytes_per_env_step.restype = ctypes.c_double
     L.f16env_last_error.restype = ctypes.c_char_p
@@ -85,6 +88,6 @@ def check(status: int, what: str):
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_get_state",
-    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant",
+    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
 )

@@ -5,6 +5,7 @@
 // (:172-197 frame, :237-261 reward/termination, :487-509 shaping, TimeLimit, Monitor
 // stats) and the DummyVecEnv auto-reset (dummy_vec_env.py:56-73) for lanes that finished,
 // with the ordered K-frame stack rebuilt by a coalesced per-wave row copy.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -14,6 +15,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/f16env.h"
 #include "f16_device.h"
@@ -1079,6 +1081,10 @@ struct f16env {
   int lds_image;   // step kernel stack-rebuild mode (LDS image when it fits)
   int gt;          // 1: the global-table step kernel (the image needs all of LDS, large K)
   size_t dyn_lds;  // dynamic LDS bytes per step-kernel block
+  // kernel timing (f16env_profile_begin/end): start/stop events recorded by the step
+  // kernel's own dispatch (hipExtLaunchKernel), one pair per launch
+  std::vector<hipEvent_t> prof_ev;
+  int prof_next = 0;
 };
 
 static void soa_carve(void* base, int64_t n, SoA& s) {
@@ -1279,6 +1285,38 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   return 0;
 }
 
+static void prof_free(f16env* h) {
+  for (hipEvent_t e : h->prof_ev) hipEventDestroy(e);
+  h->prof_ev.clear();
+  h->prof_next = 0;
+}
+
+int f16env_profile_begin(f16env_t h, int max_launches) {
+  if (!h || max_launches <= 0 || max_launches > 100000) return set_err(-1, "max_launches must be in [1, 100000]");
+  prof_free(h);
+  h->prof_ev.resize((size_t)2 * max_launches);
+  for (auto& e : h->prof_ev) HIPCHK(hipEventCreate(&e));
+  return 0;
+}
+
+int f16env_profile_end(f16env_t h, double* avg_ms, double* min_ms, int* launches) {
+  if (!h) return set_err(-1, "null handle");
+  const int n = h->prof_next;
+  double sum = 0.0, mn = 0.0;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipEventSynchronize(h->prof_ev[2 * i + 1]));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, h->prof_ev[2 * i], h->prof_ev[2 * i + 1]));
+    sum += ms;
+    mn = (i == 0 || ms < mn) ? ms : mn;
+  }
+  if (avg_ms) *avg_ms = n ? sum / n : 0.0;
+  if (min_ms) *min_ms = mn;
+  if (launches) *launches = n;
+  prof_free(h);
+  return 0;
+}
+
 int f16env_destroy(f16env_t h) {
   if (!h) return 0;
   hipSetDevice(h->device);
@@ -1286,6 +1324,7 @@ int f16env_destroy(f16env_t h) {
   hipFree(h->tmem);
   hipFree(h->ic_dev);
   if (h->done_buf) hipFree(h->done_buf);
+  prof_free(h);
   delete h;
   return 0;
 }
@@ -1339,8 +1378,13 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   }
   if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  hipLaunchKernelGGL(step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0), slot != nullptr), grid, blk,
-                     h->dyn_lds, st, a);
+  const StepKernel kern = step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0), slot != nullptr);
+  if (h->prof_next < (int)h->prof_ev.size() / 2) {  // profiling: events from the dispatch packet itself
+    const int i = h->prof_next++;
+    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)h->dyn_lds, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u, a);
+  } else {
+    hipLaunchKernelGGL(kern, grid, blk, h->dyn_lds, st, a);
+  }
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;

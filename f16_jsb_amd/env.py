@@ -191,6 +191,16 @@ class F16Envs:
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
+    def profile_kernel(self, fn, launches: int):
+        """Run fn() (which issues `launches` steps) with the step kernel's own dispatch events
+        recording each launch; returns (avg_ms, min_ms, launches timed)."""
+        L = lib()
+        check(L.f16env_profile_begin(self._h, int(launches)), "f16env_profile_begin")
+        fn()
+        avg, mn, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        check(L.f16env_profile_end(self._h, ctypes.byref(avg), ctypes.byref(mn), ctypes.byref(cnt)), "f16env_profile_end")
+        return avg.value, mn.value, cnt.value
+
     def get_state(self):
         s = self.torch.zeros((self.n, F16C_N), dtype=self.torch.float64, device=self.device)
         check(lib().f16env_get_state(self._h, self._stream(), _ptr(s)), "f16env_get_state")

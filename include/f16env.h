@@ -267,6 +267,15 @@ int f16env_step_waves_per_simd(f16env_t h);
 int f16env_step_variant(f16env_t h);
 double f16env_algorithmic_bytes_per_env_step(int stack_k);
 
+/* Kernel-duration profiling of the step: after f16env_profile_begin(h, n) the next n step
+ * launches of the handle record start/stop events from their own dispatch packets
+ * (hipExtLaunchKernel), i.e. the kernel's execution without the dependent-launch boundary;
+ * f16env_profile_end waits for them and returns the average / minimum duration (ms) and the
+ * number of launches timed. Used by bench.py for the roofline's kernel time (rocprofv3's
+ * kernel-trace average measures the same interval). */
+int f16env_profile_begin(f16env_t h, int max_launches);
+int f16env_profile_end(f16env_t h, double* avg_ms, double* min_ms, int* launches);
+
 const char* f16env_last_error(void);
 
 #ifdef __cplusplus
