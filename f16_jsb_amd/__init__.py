@@ -7,11 +7,11 @@ Soham4001A/F16_JSB: jsbsim_gym.JSBSimEnv.step()/reset() behind the SB3 VecEnv bo
 from .abi import (F16C_N, F16_IC_N, F16_OBS_DIM, EnvConfig, config_default)  # noqa: F401
 from .spaces import action_space, observation_space  # noqa: F401
 
-__all__ = ["F16Envs", "F16VecEnv", "make", "reference_goal", "config_default"]
+__all__ = ["F16Envs", "F16VecEnv", "F16GymVectorEnv", "make", "make_vec", "reference_goal", "config_default"]
 
 
 def __getattr__(name):  # lazy: importing the package must not require torch / a GPU
-    if name in ("F16Envs", "F16VecEnv", "reference_goal", "StepOut"):
+    if name in ("F16Envs", "F16VecEnv", "F16GymVectorEnv", "reference_goal", "StepOut"):
         from . import env
         return getattr(env, name)
     raise AttributeError(name)
@@ -24,3 +24,12 @@ def make(env_id: str = "JSBSim-v0", num_envs: int = 1, **kw):
         raise KeyError("unknown env id %r (only 'JSBSim-v0')" % env_id)
     from .env import F16VecEnv
     return F16VecEnv(num_envs=num_envs, **kw)
+
+
+def make_vec(env_id: str = "JSBSim-v0", num_envs: int = 1, **kw):
+    """gymnasium.make_vec("JSBSim-v0", num_envs) counterpart: the gymnasium VectorEnv surface
+    (F16GymVectorEnv, autoreset SAME_STEP) over the same kernel."""
+    if env_id != "JSBSim-v0":
+        raise KeyError("unknown env id %r (only 'JSBSim-v0')" % env_id)
+    from .env import F16GymVectorEnv
+    return F16GymVectorEnv(num_envs=num_envs, **kw)

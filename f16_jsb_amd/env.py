@@ -370,3 +370,80 @@ class F16VecEnv:
     @property
     def unwrapped(self):
         return self
+
+
+class F16GymVectorEnv:
+    """gymnasium.vector.VectorEnv surface over the same kernel (the north star's "Gymnasium
+    VectorEnv step()/reset()"), for gymnasium-native learners; duck-typed (gymnasium is not a
+    dependency). Autoreset mode SAME_STEP -- what the kernel does: a lane that terminates or
+    truncates returns its reset observation in the same step, and
+
+      infos["final_obs"] / infos["_final_obs"]   final (K,15) observation / mask
+      infos["episode"] = {"r", "l", "t"}, infos["_episode"]   (RecordEpisodeStatistics keys)
+
+    are filled for the finished lanes (gymnasium's vector-info convention: a value array plus a
+    "_key" boolean mask). ``reset(seed=s)`` seeds env i with s + i (the reference's
+    default_rng(seed) goal, jsbsim_gym.py:312-323). Single-env semantics are jsbsim_gym.py's
+    JSBSimEnv wrapped in TimeLimit(1200) and PositionReward(1e-2) (jsbsim_gym.py:537-545)."""
+
+    metadata = {"autoreset_mode": "SameStep", "render_modes": []}
+
+    def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
+                 return_numpy: bool = True, **kw):
+        self.num_envs = int(num_envs)
+        self.envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
+        self.single_observation_space = spaces.observation_space(stack_k)
+        self.single_action_space = spaces.action_space()
+        self.observation_space = spaces.batch_space(self.single_observation_space, self.num_envs)
+        self.action_space = spaces.batch_space(self.single_action_space, self.num_envs)
+        self.render_mode = None
+        self.spec = None
+        self.closed = False
+        self.return_numpy = bool(return_numpy)
+        self._t_start = time.time()
+
+    def _out(self, t):
+        return t.cpu().numpy() if self.return_numpy else t
+
+    def reset(self, *, seed=None, options=None):
+        goals = None
+        if seed is not None:
+            seeds = [seed + i for i in range(self.num_envs)] if isinstance(seed, int) else list(seed)
+            if len(seeds) != self.num_envs:
+                raise ValueError("need one seed per env")
+            if any(s is None for s in seeds):
+                self.envs.reset()
+                dev_goals = self.envs.get_state()[:, 62:65].float().cpu().numpy()
+            goals = np.stack([reference_goal(s) if s is not None else dev_goals[i] for i, s in enumerate(seeds)])
+        obs = self.envs.reset(goals=goals)
+        self._t_start = time.time()
+        return self._out(obs), {}
+
+    def step(self, actions):
+        out = self.envs.step(actions)
+        term, trunc = out.terminated.bool(), out.truncated.bool()
+        done = term | trunc
+        infos = {}
+        if bool(done.any()):
+            t = round(time.time() - self._t_start, 6)
+            mask = done.cpu().numpy()
+            infos["final_obs"] = self._out(out.terminal_obs.clone())
+            infos["_final_obs"] = mask
+            eret = out.ep_return.cpu().numpy()
+            elen = out.ep_len.cpu().numpy()
+            infos["episode"] = {"r": np.where(mask, np.round(eret, 6), 0.0), "l": np.where(mask, elen, 0),
+                                "t": np.where(mask, t, 0.0)}
+            infos["_episode"] = mask
+        return self._out(out.obs), self._out(out.rew), self._out(term), self._out(trunc), infos
+
+    def close(self, **kwargs):
+        if not self.closed:
+            self.envs.close()
+            self.closed = True
+
+    def render(self):
+        return None
+
+    @property
+    def unwrapped(self):
+        return self

@@ -77,3 +77,9 @@ def observation_space(stack_k: int = 10) -> "Box":
 
 def action_space() -> "Box":
     return Box(low=ACT_LOW, high=ACT_HIGH, shape=(4,), dtype=np.float32)
+
+
+def batch_space(space: "Box", n: int) -> "Box":
+    """gymnasium.vector.utils.batch_space for a Box: the (n, *shape) Box of n copies."""
+    return Box(low=np.broadcast_to(space.low, (n,) + space.shape), high=np.broadcast_to(space.high, (n,) + space.shape),
+               shape=(n,) + space.shape, dtype=space.dtype)

@@ -368,3 +368,48 @@ def test_cfg2_trimmed_level_flight_4096(torch_mod):
             tol = TOL_STEP * 4 if t <= 10 else (TOL_CONST300 if t == 100 else tol_long)
             _assert_frames(out.obs.cpu().numpy()[live, -1], o_r[live, -1], tol, "cfg2 trimmed @%d" % t)
     assert np.median(np.abs(o_r[ok, -1, 2] - h0[ok])) < 30.0
+
+
+def test_gymnasium_vector_env_contract(torch_mod):
+    """gymnasium VectorEnv surface (F16GymVectorEnv, autoreset SAME_STEP): batched spaces,
+    reset(seed=s) seeds env i with s + i (reference goals, bit-exact), step -> (obs, rew,
+    terminated, truncated, infos) with final_obs / episode + their "_" masks on the lanes that
+    finished, and the same transitions as the SB3 VecEnv over the same kernel."""
+    import f16_jsb_amd
+    from f16_jsb_amd import F16VecEnv, reference_goal
+    n = 16
+    env = f16_jsb_amd.make_vec("JSBSim-v0", num_envs=n, stack_k=4, seed=0, max_steps=7)
+    sb3 = F16VecEnv(num_envs=n, stack_k=4, seed=0, max_steps=7)
+    assert env.single_observation_space.shape == (4, 15) and env.observation_space.shape == (n, 4, 15)
+    assert env.single_action_space.shape == (4,) and env.action_space.shape == (n, 4)
+    assert env.metadata["autoreset_mode"] == "SameStep"
+    obs, info = env.reset(seed=42)
+    sb3.seed(42)
+    obs_s = sb3.reset()
+    assert info == {} and obs.shape == (n, 4, 15) and obs.dtype == np.float32
+    for i in range(n):
+        np.testing.assert_array_equal(obs[i, 0, 12:], reference_goal(42 + i))
+    np.testing.assert_array_equal(obs, obs_s)
+    act = np.tile(np.array([[0.1, -0.1, 0.0, 0.7]], np.float32), (n, 1))
+    finished = 0
+    for t in range(15):
+        obs, rew, term, trunc, infos = env.step(act)
+        obs_s, rew_s, dones_s, infos_s = sb3.step(act)
+        np.testing.assert_array_equal(obs, obs_s)
+        np.testing.assert_array_equal(rew, rew_s)
+        done = term | trunc
+        np.testing.assert_array_equal(done, dones_s)
+        assert term.dtype == bool and trunc.dtype == bool and rew.dtype == np.float32
+        if done.any():
+            assert set(infos) == {"final_obs", "_final_obs", "episode", "_episode"}
+            np.testing.assert_array_equal(infos["_final_obs"], done)
+            for i in np.flatnonzero(done):
+                np.testing.assert_array_equal(infos["final_obs"][i], infos_s[i]["terminal_observation"])
+                assert infos["episode"]["l"][i] == infos_s[i]["episode"]["l"]
+                assert infos["episode"]["r"][i] == infos_s[i]["episode"]["r"]
+                finished += 1
+        else:
+            assert infos == {}
+    assert finished >= 2 * n  # truncation at 7 steps
+    env.close()
+    sb3.close()
