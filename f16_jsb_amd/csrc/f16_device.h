@@ -258,6 +258,12 @@ __device__ __forceinline__ float fatan2(float y, float x) {
   return copysignf(r, y);
 }
 
+// 1-D lookup with a wave-uniform shortcut past the last interior breakpoint (every lane
+// above bp[N-2]: the segment is the last one, no search) -- the ground-effect table, whose
+// argument h/b is above 1.1 for any aircraft more than ~33 ft up
+template <int N>
+__device__ __forceinline__ float tab1_fast_end(const float (&bp)[N], const float* pairs, const float* vd, float x);
+
 // blend with a precomputed slope: v + f (v_next - v), the slope stored beside the value in
 // the blob (tools/gen_tables.py), i.e. the same fp32 FMA as lerp1 without the subtraction
 __device__ __forceinline__ float blend(float f, float v, float slope) { return __builtin_fmaf(f, slope, v); }
@@ -275,6 +281,22 @@ __device__ __forceinline__ float tab1(const float (&bp)[N], const float* pairs, 
   const Seg s = bracket(bp, pairs, x);
   const float2 p = reinterpret_cast<const float2*>(vd)[s.i - 1];
   return blend(s.f, p.x, p.y);
+}
+template <int N>
+__device__ __forceinline__ float tab1_fast_end(const float (&bp)[N], const float* pairs, const float* vd, float x) {
+  if (__ballot(!(x > bp[N - 2])) == 0) {  // same segment and factor as bracket() would give
+    const float2 q = reinterpret_cast<const float2*>(pairs)[N - 2];
+    const float f = fminf(fmaxf((x - q.x) * q.y, 0.0f), 1.0f);
+    const float2 p = reinterpret_cast<const float2*>(vd)[N - 2];
+    return blend(f, p.x, p.y);
+  }
+  return tab1(bp, pairs, vd, x);
+}
+// beta7's breakpoints are beta13's even-indexed ones, so its bracket follows from beta13's
+constexpr bool beta7_is_even_beta13() {
+  for (int j = 0; j < F16_N_B7; ++j)
+    if (BP_beta7_bp[j] != BP_beta13_bp[2 * j]) return false;
+  return 2 * (F16_N_B7 - 1) == F16_N_B13 - 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -754,7 +776,14 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     const f2v r = blend2(sb13.f, c1, c2 - c1);
     AB13[0] = r.x; AB13[1] = r.y;
   }
-  const Seg sb7 = bracket(BP_beta7_bp, T + OFF_pair_beta7, a.beta);
+  // i7 - 1 = #{even-indexed interior beta13 breakpoints below beta} = (i13 - 1) / 2
+  static_assert(beta7_is_even_beta13(), "beta7 grid must be the even beta13 breakpoints");
+  Seg sb7;
+  {
+    sb7.i = 1 + ((sb13.i - 1) >> 1);
+    const float2 p = reinterpret_cast<const float2*>(T + OFF_pair_beta7)[sb7.i - 1];
+    sb7.f = fminf(fmaxf((a.beta - p.x) * p.y, 0.0f), 1.0f);
+  }
   float AB7[4];  // Clda, Cldr, Cnda, Cndr over (alpha, beta 7)
   {
     const float* p0 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 8;
@@ -910,7 +939,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   ai.qbar = qbar; ai.alpha = alpha; ai.beta = beta; ai.mach = mach;
   ai.p = d.pqr[0]; ai.q = d.pqr[1]; ai.r = d.pqr[2];
   ai.bi2vel = bi2vel; ai.ci2vel = ci2vel;
-  ai.kclge = tab1(BP_kclge, T + OFF_pair_kclge, T + OFF_kclge_vd, hbmac);
+  ai.kclge = tab1_fast_end(BP_kclge, T + OFF_pair_kclge, T + OFF_kclge_vd, hbmac);
   ai.de = fc.de; ai.da = fc.da; ai.dr = fc.dr; ai.dlef = fc.dlef; ai.flap = fc.flap_mix; ai.dsb = fc.dsb;
   float A6[6];
   aero(ai, T, A6);
