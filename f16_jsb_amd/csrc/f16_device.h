@@ -156,10 +156,12 @@ template <bool GUST = false>
 __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   const int64_t n = s.n;
   float4 c[NCOL];
+  // column pointers by increment (one 64-bit scalar add per column, not a 64-bit multiply)
+  const float4* p = s.c + k;
 #pragma unroll
-  for (int j = 0; j < NCOL; ++j) c[j] = s.c[j * n + k];
+  for (int j = 0; j < NCOL; ++j, p += n) c[j] = *p;
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (GUST) g = s.c[COL_GUST * n + k];
+  if (GUST) g = *p;
   lane_unpack<GUST>(c, g, L);
 }
 // the one-env IC template staged in LDS (columns contiguous): no vector-memory traffic, so
@@ -195,9 +197,10 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   c[17] = GUST ? make_float4(L.last_d, L.wst[0], L.wst[1], L.wst[2])
                : make_float4(L.last_d, L.wind[0], L.wind[1], L.wind[2]);
   c[18] = make_float4(__int_as_float(L.step), __int_as_float(L.ep_count), __int_as_float(L.flags), 0.0f);
+  float4* p = s.c + k;
 #pragma unroll
-  for (int j = 0; j < NCOL; ++j) s.c[j * n + k] = c[j];
-  if (GUST) s.c[COL_GUST * n + k] = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
+  for (int j = 0; j < NCOL; ++j, p += n) *p = c[j];
+  if (GUST) *p = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -217,9 +220,20 @@ __device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_a
 // 1-D end clamps coincide with it).
 template <int N>
 __device__ __forceinline__ Seg bracket(const float (&bp)[N], const float* pairs, float x) {
+#ifdef F16_BRACKET_CMP
   int i = 1;
 #pragma unroll
   for (int k = 1; k < N - 1; ++k) i += (bp[k] < x) ? 1 : 0;
+#else
+  // bp[k] < x  <=>  sign bit of the fp32 difference bp[k] - x (exact in sign: a difference
+  // of finite floats rounds to zero only when they are equal, and +0 for x == bp[k]). Counting
+  // sign bits keeps the count in VALU integer ops; the compare form costs a VCC write, an
+  // SGPR literal and an s_nop hazard pad per breakpoint on gfx950.
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 1; k < N - 1; ++k) c += __float_as_uint(bp[k] - x) >> 31;
+  const int i = 1 + (int)c;
+#endif
   const float2 p = reinterpret_cast<const float2*>(pairs)[i - 1];
   float f = (x - p.x) * p.y;
   f = fminf(fmaxf(f, 0.0f), 1.0f);
@@ -900,9 +914,11 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const float muw = ua * ua + wa * wa;
   const float vt = fsqrt(muw + va * va);
   const bool moving = muw > 0.0f;
-  const float alpha = moving ? fatan2(wa, ua) : 0.0f;
+  // JSBSim's alpha = beta = 0 when not moving, as fatan2(+0, 0) = +0 on guarded inputs:
+  // straight-line code instead of two divergent branches around the polynomials
+  const float alpha = fatan2(moving ? wa : 0.0f, ua);
   const float suw = fsqrt(muw);
-  const float beta = moving ? fatan2(va, suw) : 0.0f;
+  const float beta = fatan2(moving ? va : 0.0f, suw);
   const float iuw = rcpf(suw), ivt = rcpf(vt);
   const float ca_ = moving ? ua * iuw : 1.0f, sa_ = moving ? wa * iuw : 0.0f;
   const float cb_ = moving ? suw * ivt : 1.0f, sb_ = moving ? va * ivt : 0.0f;

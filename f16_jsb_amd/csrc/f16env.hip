@@ -315,6 +315,11 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
 }
 
+// The template's frame 0 without the goal (12 floats) follows its NCOL_ALL state columns as
+// TMPL_FRAME_COLS float4s, written once by f16_ic_kernel with the same make_frame: an
+// auto-reset then costs the goal draw only, not a frame evaluation (fp64 altitude, Euler
+// angles, atan2s) on the critical path of every wave that holds a finished lane.
+enum { TMPL_FRAME_COLS = 3, TMPL_COLS = NCOL_ALL + TMPL_FRAME_COLS };
 __device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl, const EnvArgs& E, int64_t k,
                                                     float* f0) {
   const int32_t ep = L.ep_count;
@@ -323,7 +328,16 @@ __device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
+#ifdef F16_RESET_MAKE_FRAME  // A/B only: evaluate frame 0 per finished lane
   make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
+#else
+#pragma unroll
+  for (int j = 0; j < TMPL_FRAME_COLS; ++j) {
+    const float4 v = sTmpl[NCOL + j];
+    f0[4 * j] = v.x; f0[4 * j + 1] = v.y; f0[4 * j + 2] = v.z; f0[4 * j + 3] = v.w;
+  }
+  f0[12] = L.goal[0]; f0[13] = L.goal[1]; f0[14] = L.goal[2];
+#endif
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
 }
 
@@ -334,6 +348,14 @@ __device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl
 #define BLOCK 256
 #endif
 #define FRAME_PITCH 16
+// The previous stack block lands in the wave's LDS image IMG_OFF floats past its 16-byte
+// aligned base. IMG_OFF = 1 makes the shifted copy-out out[j] = img[IMG_OFF + j + 15] whole
+// aligned float4s (ds_read_b128 instead of four dwords), but the misaligned LDS-DMA landing
+// costs more than it saves (measured 23.0 vs 23.3 us per step at 65 536 envs, K = 4; 31.2 vs
+// 32.3 at K = 10: profiles/r01_variants_w.json), so the image stays aligned.
+#ifndef IMG_OFF
+#define IMG_OFF 0
+#endif
 
 // LDS-DMA of 16 B per lane: lane i's 16 bytes land at lds + 16*i (gfx950 global_load_lds_dwordx4)
 __device__ __forceinline__ void dma16(const float* g, float* lds) {
@@ -424,9 +446,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       const int n16 = total >> 2;   // whole 16-byte pieces (wave blocks are 16-B aligned)
       for (int b = 0; b < n16; b += 64) {
         const int piece = b + lane;
-        if (piece < n16) dma16(prev + 4 * piece, img + 4 * b);
+        if (piece < n16) dma16(prev + 4 * piece, img + IMG_OFF + 4 * b);
       }
-      if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + 4 * n16);  // tail, never past the end
+      if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + IMG_OFF + 4 * n16);  // tail, never past the end
     }
   };
 #if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && defined(F16_DMA_FIRST)
@@ -442,8 +464,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // (only needed by the obs rebuild) is DMA'd after that wait, so it streams in while the
   // first frame runs instead of sharing the prologue's HBM bandwidth.
   if (!GT) stage_tables_issue(sT_lds);
-  if (!DEFER && threadIdx.x < NCOL) dma16(reinterpret_cast<const float*>(a.tmpl.c + threadIdx.x),
-                                          reinterpret_cast<float*>(sTmpl));
+  // IC template: the NCOL state columns, then its frame-0 columns (lane i lands at sTmpl[i])
+  if (!DEFER && threadIdx.x < NCOL + TMPL_FRAME_COLS)
+    dma16(reinterpret_cast<const float*>(a.tmpl.c + (threadIdx.x < NCOL ? threadIdx.x : threadIdx.x + NCOL_ALL - NCOL)),
+          reinterpret_cast<float*>(sTmpl));
   if (live) {
     lane_load<GUST>(a.s, k, L);
     if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
@@ -569,14 +593,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int j = 4 * q + i, r = j / F16_OBS_DIM, c = j - r * F16_OBS_DIM;
-            v[i] = img[r * KC + HC + c];
+            v[i] = img[IMG_OFF + r * KC + HC + c];
           }
           reinterpret_cast<float4*>(dst)[q] = make_float4(v[0], v[1], v[2], v[3]);
         }
       } else {
         for (int j = lane; j < rows * F16_OBS_DIM; j += 64) {
           const int r = j / F16_OBS_DIM, c = j - r * F16_OBS_DIM;
-          dst[j] = img[r * KC + HC + c];
+          dst[j] = img[IMG_OFF + r * KC + HC + c];
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -593,14 +617,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     //    below need no workgroup barrier (a wave's LDS accesses complete in order).
     __builtin_amdgcn_wave_barrier();
     if (live) {
-      float* dst = img + (size_t)(lane + 1) * KC;
+      float* dst = img + IMG_OFF + (size_t)(lane + 1) * KC;
 #pragma unroll
       for (int j = 0; j < F16_OBS_DIM; ++j) dst[j] = f[j];
     }
     __builtin_amdgcn_wave_barrier();
     // 3) finished rows: terminal obs = the spliced row; then the row becomes K x frame 0
     if (live && done) {
-      float* src = img + (size_t)lane * KC + F16_OBS_DIM;
+      float* src = img + IMG_OFF + (size_t)lane * KC + F16_OBS_DIM;
       if (a.tobs) {
         float* t = a.tobs + k * KC;
         for (int c = 0; c < KC; ++c) t[c] = src[c];
@@ -617,11 +641,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       float4* out4 = reinterpret_cast<float4*>(out);
 #ifndef F16_DIAG_SKIP_COPYOUT
       for (int q = lane; q < n4; q += 64) {
-        const float* p = img + 4 * q + F16_OBS_DIM;
+#if (IMG_OFF + F16_OBS_DIM) % 4 == 0
+        out4[q] = reinterpret_cast<const float4*>(img + IMG_OFF + F16_OBS_DIM)[q];
+#else
+        const float* p = img + IMG_OFF + 4 * q + F16_OBS_DIM;
         out4[q] = make_float4(p[0], p[1], p[2], p[3]);
+#endif
       }
 #endif
-      for (int j = 4 * n4 + lane; j < total; j += 64) out[j] = img[j + F16_OBS_DIM];
+      for (int j = 4 * n4 + lane; j < total; j += 64) out[j] = img[IMG_OFF + j + F16_OBS_DIM];
     }
     F16_STAMP(stamps, ST_COPY);
   } else {
@@ -695,7 +723,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
 
 #define STEP_SHARED                                       \
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];   \
-  __shared__ __align__(16) float4 sTmpl[NCOL];            \
+  __shared__ __align__(16) float4 sTmpl[NCOL + TMPL_FRAME_COLS]; \
   __shared__ int sDone[BLOCK];                            \
   extern __shared__ __align__(16) float dynl[];
 
@@ -715,7 +743,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
 // global-table variant (large K on the LDS-image path): no LDS table copy
 template <int MODE, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
-  __shared__ __align__(16) float4 sTmpl[NCOL];
+  __shared__ __align__(16) float4 sTmpl[NCOL + TMPL_FRAME_COLS];
   __shared__ int sDone[BLOCK];
   extern __shared__ __align__(16) float dynl[];
   step_body<MODE, true, ROLL>(a, nullptr, sTmpl, sDone, dynl);
@@ -805,6 +833,11 @@ __global__ void f16_ic_kernel(SoA dst, const double* ic, ModelConsts C) {
   L.ep_ret = 0.0; L.step = 0; L.ep_count = 0; L.last_d = 0.0f;
   L.goal[0] = L.goal[1] = L.goal[2] = 0.0f;
   lane_store(dst, 0, L);
+  // frame 0 of the template (goal excluded): what every template auto-reset would evaluate
+  float f[F16_OBS_DIM];
+  make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f);
+  for (int j = 0; j < TMPL_FRAME_COLS; ++j)
+    dst.c[NCOL_ALL + j] = make_float4(f[4 * j], f[4 * j + 1], f[4 * j + 2], f[4 * j + 3]);
 }
 
 __global__ void f16_get_state_kernel(SoA s, double* c) {
@@ -1230,7 +1263,7 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   soa_carve(h->mem, cfg->n_envs, h->soa);
   h->mode = ((cfg->flags & F16_FLAG_RANDOM_IC) ? 1 : 0) | ((cfg->flags & F16_FLAG_GUSTS) ? 2 : 0);
   h->done_buf = nullptr;
-  if (hipMalloc(&h->tmem, soa_bytes(1)) != hipSuccess ||
+  if (hipMalloc(&h->tmem, (size_t)TMPL_COLS * 16) != hipSuccess ||
       hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||
       (h->mode && hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 1)) != hipSuccess)) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
@@ -1241,7 +1274,7 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const int KC = cfg->stack_k * F16_OBS_DIM;
     const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
     const size_t fallback = sizeof(float) * 2 * BLOCK * FRAME_PITCH;
-    const size_t static_gt = 16 * NCOL + sizeof(int) * BLOCK + 64;
+    const size_t static_gt = 16 * (NCOL + TMPL_FRAME_COLS) + sizeof(int) * BLOCK + 64;
     const size_t static_lds = sizeof(float) * F16_BLOB_FLOATS + static_gt;
     // the stack image with LDS tables if both fit, else with global tables, else the
     // chunked flat copy (LDS tables)

@@ -177,6 +177,35 @@ def test_autoreset_crash_parity(torch_mod):
     assert saw.all()
 
 
+def test_autoreset_frame_equals_reset_kernel_frame(torch_mod):
+    """The step kernel's auto-reset copies frame 0 of the IC template, evaluated once at create
+    (f16_ic_kernel); f16env_reset evaluates it per lane (f16_reset_kernel). For the same IC
+    and goal both give the same K x 15 rows, bit for bit."""
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    n = 512
+    ic = np.tile(default_ic(), (n, 1))
+    ic[:, 2] = np.linspace(150.0, 900.0, n)   # ft
+    ic[:, 7] = -0.6                           # dive: every lane crashes within ~2 s
+    g = F16Envs(n, stack_k=4, seed=21)
+    g.reset(ic=ic)
+    act = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    seen = 0
+    for t in range(80):
+        out = g.step(act)
+        d = (out.terminated | out.truncated).bool()
+        if not bool(d.any()):
+            continue
+        auto = out.obs[d].clone()
+        assert torch.equal(auto, auto[:, :1].expand_as(auto))
+        goals = out.obs[:, 0, 12:15].contiguous()
+        r = g.reset(mask=d, goals=goals)          # rewrites the same rows in place
+        assert torch.equal(r[d], auto)
+        seen += int(d.sum())
+    assert seen >= n // 2
+    g.close()
+
+
 def test_trim_parity_and_level_flight(torch_mod):
     torch = torch_mod
     n = 16
