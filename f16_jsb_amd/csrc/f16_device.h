@@ -332,10 +332,16 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   const float z = h_ft * 0.3048f;
   const float H = 6356766.0f * z * rcpf(6356766.0f + z);
   constexpr float EX[7] = {GMR / Lb[0], 0.0f, GMR / Lb[2], GMR / Lb[3], 0.0f, GMR / Lb[5], GMR / Lb[6]};
-  float hb = Hb[0], lb = Lb[0], tb = Tb[0], pb = Pb[0], ex = EX[0];
+  // P = pb (tb/T)^ex in the gradient layers, pb exp(-GMR (H - hb) / tb) in the isothermal
+  // ones: both as one v_log_f32 + one v_exp_f32 (OCML powf is ~130 VALU of compensated
+  // double-float arithmetic; v_log/v_exp keep P within ~1e-7 relative)
+  float T, lg2, pb;
   // layer search only when some lane of the wave is above the troposphere (wave-uniform
-  // branch; the reference task and the cfg5 IC box stay below 11 km almost always)
+  // branch; the reference task and the cfg5 IC box stay below 11 km almost always); the
+  // troposphere path has its layer constants as literals
   if (__builtin_expect(__ballot(H >= Hb[1]) != 0, 0)) {
+    float hb = Hb[0], lb = Lb[0], tb = Tb[0], ex = EX[0];
+    pb = Pb[0];
     int b = 0;
 #pragma unroll
     for (int k = 1; k < 7; ++k) b += (H >= Hb[k]) ? 1 : 0;
@@ -343,13 +349,14 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
     for (int k = 1; k < 7; ++k) {
       if (b == k) { hb = Hb[k]; lb = Lb[k]; tb = Tb[k]; pb = Pb[k]; ex = EX[k]; }
     }
+    T = tb + lb * (H - hb);
+    lg2 = (lb != 0.0f) ? ex * __builtin_amdgcn_logf(tb * rcpf(T))
+                       : (-GMR * 1.4426950408889634f) * (H - hb) * rcpf(tb);
+  } else {
+    T = Tb[0] + Lb[0] * H;  // hb = 0
+    lg2 = EX[0] * __builtin_amdgcn_logf(Tb[0] * rcpf(T));
+    pb = Pb[0];
   }
-  // P = pb (tb/T)^ex in the gradient layers, pb exp(-GMR (H - hb) / tb) in the isothermal
-  // ones: both as one v_log_f32 + one v_exp_f32, branch-free (OCML powf is ~130 VALU of
-  // compensated double-float arithmetic; v_log/v_exp keep P within ~1e-7 relative)
-  const float T = tb + lb * (H - hb);
-  const float lg2 = (lb != 0.0f) ? ex * __builtin_amdgcn_logf(tb * rcpf(T))
-                                 : (-GMR * 1.4426950408889634f) * (H - hb) * rcpf(tb);
   const float P = pb * __builtin_amdgcn_exp2f(lg2);
   const float rho = P * rcpf(R * T);
   Atm o;
