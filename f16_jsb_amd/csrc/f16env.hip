@@ -68,8 +68,10 @@ __device__ __forceinline__ void rng_goal(uint64_t seed, uint64_t gid, uint32_t e
   const double dist = 1000.0 + (10000.0 - 1000.0) * u53(o[0], o[1]);
   const double bear = 0.0 + (2.0 * PI_D - 0.0) * u53(o[2], o[3]);
   const double alt = 1000.0 + (4000.0 - 1000.0) * u53(o2[0], o2[1]);
-  g[0] = (float)(dist * cos(bear));
-  g[1] = (float)(dist * sin(bear));
+  double sb, cb;
+  sincos(bear, &sb, &cb);  // one argument reduction for both (same values as cos / sin)
+  g[0] = (float)(dist * cb);
+  g[1] = (float)(dist * sb);
   g[2] = (float)alt;
 }
 
@@ -627,10 +629,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       float* src = img + IMG_OFF + (size_t)lane * KC + F16_OBS_DIM;
       if (a.tobs) {
         float* t = a.tobs + k * KC;
-        for (int c = 0; c < KC; ++c) t[c] = src[c];
+        if ((KC & 3) == 0) {  // K % 4 == 0: the row is 16-B aligned in HBM, dwordx4 stores
+          for (int c = 0; c < KC; c += 4)
+            *reinterpret_cast<float4*>(t + c) = make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]);
+        } else {
+          for (int c = 0; c < KC; ++c) t[c] = src[c];
+        }
       }
-      if (autoreset)
-        for (int c = 0; c < KC; ++c) src[c] = f0[c % F16_OBS_DIM];
+      if (autoreset)  // frame by frame: f0 indexed by literals (no per-element modulo / select chain)
+        for (int r = 0; r < a.E.K; ++r)
+#pragma unroll
+          for (int j = 0; j < F16_OBS_DIM; ++j) src[r * F16_OBS_DIM + j] = f0[j];
     }
     __builtin_amdgcn_wave_barrier();
     F16_STAMP(stamps, ST_SYNC);
