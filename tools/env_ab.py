@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of step-kernel variants selected by environment variables at handle creation
-(F16ENV_OCC, F16ENV_GT; F16ENV_HALF selected the half-wave layout measured in profiles/r01_env_ab_half.json, since removed), one process, same library. Run on the GPU box:
+(F16ENV_OCC, F16ENV_GT; F16ENV_HALF and F16ENV_SPLIT selected the half-wave and two-wave-frame
+layouts measured in profiles/r01_env_ab_half.json / r01_env_ab_split.json, since removed), one process, same library. Run on the GPU box:
 
     python tools/env_ab.py [--json out.json] [--steps 300] NAME=VAR=VAL[,VAR=VAL] ...
 
@@ -15,7 +16,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-KNOBS = ("F16ENV_HALF", "F16ENV_OCC", "F16ENV_GT")
+KNOBS = ("F16ENV_OCC", "F16ENV_GT")
 SHAPES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (65536, 10, 4), (4096, 4, 4)]
 
 
