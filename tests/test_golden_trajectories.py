@@ -1,0 +1,82 @@
+"""Committed golden trajectories (tests/golden/trajectories.npz, made by
+tests/golden/make_trajectories.py from the CPU oracle on fixed inputs).
+
+* CPU: the oracle re-run on the committed inputs reproduces every committed output bit for bit
+  (pins the oracle -- the parity checker -- against drift).
+* GPU: the HIP path on the same inputs matches the committed outputs, read from the fixture
+  (no oracle run), within the tolerances of test_gpu_parity.py: done flags bit-exact, rewards
+  within 2e-3, newest frames at the checkpoints within the step / 300-step constant-action /
+  30-step random-action tolerances.
+Parity against JSBSim itself stays unpinned: the fixture is the restatement's.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+from parity_tools import frame_err
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden", "trajectories.npz")
+
+TOL_STEP = np.array([1e-3, 1e-3, 1e-3, 5e-6, 5e-6, 5e-6, 5e-5, 5e-5, 5e-5, 5e-6, 5e-6, 5e-6, 0, 0, 0])
+TOL_CONST300 = np.array([5e-2, 5e-2, 5e-2, 1e-5, 1e-5, 1e-5, 5e-5, 5e-5, 5e-5, 1e-4, 1e-4, 1e-4, 0, 0, 0])
+TOL_RAND30 = np.array([5e-3, 5e-3, 5e-3, 2e-5, 5e-5, 5e-5, 5e-4, 5e-4, 5e-4, 5e-5, 5e-5, 5e-5, 0, 0, 0])
+
+
+def _gen():
+    spec = importlib.util.spec_from_file_location("make_trajectories", os.path.join(HERE, "golden", "make_trajectories.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_oracle_reproduces_golden_trajectories(oracle_lib):
+    gold = np.load(GOLD)
+    mt = _gen()
+    for case, steps, check in (("const", 300, mt.CONST_CHECK), ("random", 30, mt.RANDOM_CHECK)):
+        f, r, d = mt.run(gold[case + "_ic"], gold[case + "_goals"], gold[case + "_act"], steps, check)
+        np.testing.assert_array_equal(f, gold[case + "_frames"], err_msg=case)
+        np.testing.assert_array_equal(r, gold[case + "_rew"], err_msg=case)
+        np.testing.assert_array_equal(d, gold[case + "_done"], err_msg=case)
+
+
+def test_golden_inputs_are_the_generator_inputs():
+    gold = np.load(GOLD)
+    mt = _gen()
+    for case, inputs in (("const", mt.const_inputs()), ("random", mt.random_inputs())):
+        for name, v in zip(("ic", "goals", "act"), inputs):
+            np.testing.assert_array_equal(gold["%s_%s" % (case, name)], v, err_msg="%s_%s" % (case, name))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["const", "random"])
+def test_gpu_matches_golden_trajectories(gpu, case):
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    gold = np.load(GOLD)
+    mt = _gen()
+    steps, check = (300, mt.CONST_CHECK) if case == "const" else (30, mt.RANDOM_CHECK)
+    acts = gold[case + "_act"]
+    n = len(gold[case + "_goals"])
+    g = F16Envs(n, stack_k=4, seed=3)
+    g.reset(goals=gold[case + "_goals"], ic=gold[case + "_ic"])
+    ta = torch.as_tensor(acts).cuda()
+    frames = []
+    for t in range(1, steps + 1):
+        out = g.step(ta if acts.ndim == 2 else ta[t - 1].contiguous())
+        done = (out.terminated | out.truncated).cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(done, gold[case + "_done"][t - 1], err_msg="done @%d" % t)
+        np.testing.assert_allclose(out.rew.cpu().numpy(), gold[case + "_rew"][t - 1], atol=2e-3, err_msg="rew @%d" % t)
+        if t in check:
+            frames.append(out.obs[:, -1].cpu().numpy())
+    g.close()
+    for i, t in enumerate(check):
+        tol = TOL_STEP * 4 if t <= 10 else (TOL_CONST300 if case == "const" else TOL_RAND30)
+        err = frame_err(frames[i], gold[case + "_frames"][i])
+        bad = np.argwhere(err > tol)
+        assert not len(bad), "%s @%d: env %d component %d err %.3e > %.1e" % (
+            case, t, bad[0][0], bad[0][1], err[tuple(bad[0])], tol[bad[0][1]])
