@@ -399,6 +399,7 @@ struct StepArgs {
   int32_t* ep_len;
   int32_t* done_idx;
   int32_t* n_done;
+  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine count (handle-owned)
   int32_t lds_image;
   // rollout slot (f16env_step_rollout; all NULL / 0 for f16env_step)
   int32_t sample_act;          // act == NULL: draw the actions in-kernel (seed, step)
@@ -512,7 +513,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     // reward / termination (:237-261) in float32, then PositionReward (:493-507)
     float r32;
     int te = 0, tr;
-    {
+    // F16_FLAG_NAN_GUARD: a non-finite position / Mach / alpha / beta / body rate (the angles
+    // f[9..11] are already NaN -> 0 by normalize_angle_mpi_pi) quarantines the lane
+    bool bad = false;
+    if (a.E.flags & F16_FLAG_NAN_GUARD) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j) bad = bad || !isfinite(f[j]);
+    }
+    if (bad) {
+      te = 5;  // terminated + quarantined (bit 2), reported as terminated[i] = 3
+      tr = 0;
+      r32 = 0.0f;
+    } else {
 #pragma clang fp contract(off)
       double r = 0.0;
       const float alt = f[2];
@@ -532,7 +544,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     F16_STAMP(stamps, ST_REWARD);
     done = te | tr;
     rew_out = r32;
-    flags_out = te | (tr << 1);
+    flags_out = te | (tr << 1);  // bit 0 terminated, 1 truncated, 2 quarantined
   }
   // the stack DMA issued after the prologue has long landed; retire it here, before any
   // store of this step (vmcnt also counts stores on CDNA, so a later wait would drain them)
@@ -548,10 +560,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
     }
   }
+  if (a.E.flags & F16_FLAG_NAN_GUARD) {
+    const unsigned long long qm = __ballot(flags_out & 4);
+    if (qm && lane == 0) atomicAdd(a.nonfinite, (unsigned long long)__popcll(qm));
+  }
   if (live) {
     a.rew[k] = rew_out;
-    a.term[k] = (uint8_t)(flags_out & 1);
-    a.trunc[k] = (uint8_t)(flags_out >> 1);
+    a.term[k] = (uint8_t)((flags_out & 1) | ((flags_out >> 1) & 2));
+    a.trunc[k] = (uint8_t)((flags_out >> 1) & 1);
     if (ROLL) {
       if (a.r_rew) a.r_rew[k] = rew_out;
       if (a.r_act) reinterpret_cast<float4*>(a.r_act)[k] = av;
@@ -1115,6 +1131,7 @@ struct f16env {
   void* tmem;      // template SoA (n = 1)
   double* ic_dev;  // default IC, RANDOM_IC box lo, hi (3 x F16_IC_N)
   int32_t* done_buf;  // deferred modes: own done list (N) + count, when the caller gives none
+  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine counter (device, 8 B)
   int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 GUSTS
   int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
   SoA soa, tmpl;
@@ -1279,6 +1296,11 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     return set_err(-3, "hipMalloc(template) failed");
   }
   soa_carve(h->tmem, 1, h->tmpl);
+  if (hipMalloc((void**)&h->nonfinite, sizeof(unsigned long long)) != hipSuccess) {
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
+    return set_err(-3, "hipMalloc(counter) failed");
+  }
+  hipMemset(h->nonfinite, 0, sizeof(unsigned long long));
   {
     const int KC = cfg->stack_k * F16_OBS_DIM;
     const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
@@ -1307,7 +1329,8 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
         if (hipFuncSetAttribute((const void*)step_kernel_for(m & 3, v, m >= 4), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dyn) != hipSuccess) {
           (void)hipGetLastError();
-          hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
+          hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); hipFree(h->nonfinite);
+          delete h;
           return set_err(-2, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         }
       }
@@ -1320,7 +1343,7 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) {
-    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); hipFree(h->nonfinite); delete h;
     return set_err(-2, hipGetErrorString(e));
   }
   *out = h;
@@ -1366,6 +1389,7 @@ int f16env_destroy(f16env_t h) {
   hipFree(h->tmem);
   hipFree(h->ic_dev);
   if (h->done_buf) hipFree(h->done_buf);
+  hipFree(h->nonfinite);
   prof_free(h);
   delete h;
   return 0;
@@ -1399,6 +1423,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   a.s = h->soa; a.tmpl = h->tmpl; a.act = act; a.obs_prev = obs_prev; a.obs = obs; a.rew = rew;
   a.term = terminated; a.trunc = truncated; a.tobs = terminal_obs; a.ep_ret = ep_return; a.ep_len = ep_len;
   a.done_idx = done_idx; a.n_done = n_done;
+  a.nonfinite = h->nonfinite;
   a.sample_act = act ? 0 : 1;
   a.act_seed = slot ? slot->act_seed : 0; a.act_step = slot ? slot->act_step : 0;
   a.r_frame = slot ? slot->frame : nullptr;
@@ -1459,6 +1484,15 @@ int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slo
   if (!slot) return set_err(-1, "null rollout slot");
   return step_impl(h, stream, slot, act, obs_prev, obs, rew, terminated, truncated, terminal_obs, ep_return,
                    ep_len, done_idx, n_done);
+}
+
+int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count) {
+  if (!h || !count) return set_err(-1, "null argument");
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, h->nonfinite, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  *count = (uint64_t)v;
+  return 0;
 }
 
 int f16env_get_state(f16env_t h, void* stream, double* canon) {

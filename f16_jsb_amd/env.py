@@ -21,7 +21,8 @@ import numpy as np
 
 from . import spaces
 from ._lib import F16EnvError, check, lib
-from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC,
+from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
+                  F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
 StepOut = namedtuple("StepOut", "obs rew terminated truncated terminal_obs ep_return ep_len")
@@ -49,7 +50,7 @@ class F16Envs:
 
     def __init__(self, n_envs: int, stack_k: int = 10, device=None, seed: int = 0,
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
-                 autoreset: bool = True, ic=None, **cfg_kw):
+                 autoreset: bool = True, ic=None, nan_guard: bool = False, **cfg_kw):
         import torch
 
         if not torch.cuda.is_available():
@@ -60,7 +61,8 @@ class F16Envs:
             raise F16EnvError("device must be a cuda (ROCm) device, got %s" % self.device)
         self.n = int(n_envs)
         self.k = int(stack_k)
-        flags = int(cfg_kw.pop("flags", 0)) | (0 if autoreset else F16_FLAG_NO_AUTORESET)
+        flags = int(cfg_kw.pop("flags", 0)) | (0 if autoreset else F16_FLAG_NO_AUTORESET) \
+            | (F16_FLAG_NAN_GUARD if nan_guard else 0)
         self.cfg: EnvConfig = config_default(n_envs=n_envs, stack_k=stack_k, seed=seed, env_id_base=env_id_base,
                                              max_steps=max_steps, down_sample=down_sample, flags=flags, ic=ic,
                                              **cfg_kw)
@@ -201,6 +203,15 @@ class F16Envs:
         check(L.f16env_profile_end(self._h, ctypes.byref(avg), ctypes.byref(mn), ctypes.byref(cnt)), "f16env_profile_end")
         return avg.value, mn.value, cnt.value
 
+    @property
+    def nonfinite_count(self) -> int:
+        """Lanes quarantined by the NaN guard (nan_guard=True) since creation; waits for the
+        handle's stream. A quarantined lane ended its step terminated (terminated == 3) with
+        reward 0 and was reset."""
+        c = ctypes.c_uint64()
+        check(lib().f16env_nonfinite_count(self._h, self._stream(), ctypes.byref(c)), "f16env_nonfinite_count")
+        return int(c.value)
+
     def get_state(self):
         s = self.torch.zeros((self.n, F16C_N), dtype=self.torch.float64, device=self.device)
         check(lib().f16env_get_state(self._h, self._stream(), _ptr(s)), "f16env_get_state")
@@ -290,7 +301,8 @@ class F16VecEnv:
             return out.obs, out.rew, dones, None
         obs = out.obs.cpu().numpy()
         rew = out.rew.cpu().numpy()
-        term = out.terminated.cpu().numpy().astype(bool)
+        term_u8 = out.terminated.cpu().numpy()
+        term = term_u8.astype(bool)
         trunc = out.truncated.cpu().numpy().astype(bool)
         dones = term | trunc
         infos = [{"TimeLimit.truncated": False} for _ in range(self.num_envs)]
@@ -304,6 +316,8 @@ class F16VecEnv:
                 infos[i]["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
                 infos[i]["terminal_observation"] = tobs[j]
                 infos[i]["episode"] = {"r": round(float(eret[j]), 6), "l": int(elen[j]), "t": t}
+                if term_u8[i] & 2:  # NaN guard quarantine (nan_guard=True)
+                    infos[i]["nonfinite"] = True
         return obs, rew, dones, infos
 
     def step(self, actions):

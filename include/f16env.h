@@ -127,6 +127,12 @@ enum f16_latch_index {
  *     from Philox keyed by (seed; gid, gid_hi ^ 0x47555354, episode, s). */
 #define F16_FLAG_RANDOM_IC 0x2
 #define F16_FLAG_GUSTS 0x4
+/* Failure detection (the reference has none -- a non-finite JSBSim state just
+ * propagates into the observation, jsbsim_gym.py:268-285 only prints): a lane whose new frame
+ * has a non-finite position, Mach, alpha, beta or body rate ends that step as terminated with
+ * reward 0 and terminated[i] = 3 (bit 1 marks the quarantine), is auto-reset like any finished
+ * lane, and is counted (f16env_nonfinite_count). Off by default. */
+#define F16_FLAG_NAN_GUARD 0x8
 
 typedef struct f16env_config {
   int32_t n_envs;       /* envs on this device                                          */
@@ -213,6 +219,9 @@ int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slo
                         const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
                         float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx,
                         int32_t* n_done);
+
+/* Lanes quarantined by F16_FLAG_NAN_GUARD since create (waits for `stream`). */
+int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);
 
 /* Canonical state export/import: canon is N x F16C_N double (device). */
 int f16env_get_state(f16env_t h, void* stream, double* canon);

@@ -1026,24 +1026,33 @@ int f16ref_step(f16ref* h, const float* act, float* obs, float* rew, uint8_t* te
     make_frame(e, f);                                               /* :234 */
     memcpy(e->stack + e->head * F16_OBS_DIM, f, sizeof f);          /* :235 deque append */
     e->head = (e->head + 1) % K_;
-    /* reward / termination (:237-261), float32 arithmetic on the frame */
+    /* F16_FLAG_NAN_GUARD (build-defined, include/f16env.h): a non-finite position, Mach,
+       alpha, beta or body rate ends the step terminated (term = 3) with reward 0 */
+    int bad = 0;
+    if (h->cfg.flags & F16_FLAG_NAN_GUARD)
+      for (int j = 0; j < 9; j++) bad |= !isfinite(f[j]);
     double r = 0.0;
-    int te = 0;
-    float alt = f[2];
-    if (alt < crash) { r = -10.0; te = 1; }
-    float dx = f[0] - f[12], dy = f[1] - f[13];
-    volatile float d2 = dx * dx;
-    d2 = d2 + dy * dy;
-    float dalt = alt - f[14];
-    if (!te && sqrtf(d2) < dg && fabsf(dalt) < dg) { r = 10.0; te = 1; }
-    int tr = e->step >= h->cfg.max_steps; /* env :260 OR gymnasium TimeLimit(1200) */
-    /* PositionReward (:493-507) */
-    float gx = f[12] - f[0], gy = f[13] - f[1], gz = f[14] - f[2];
-    float dcur = norm3f(gx, gy, gz);
-    float ddiff = e->last_d - dcur;
-    r += h->cfg.goal_gain * (double)ddiff;
-    e->last_d = dcur;
-    e->ep_ret += r;                                                 /* Monitor :96-99 */
+    int te = 0, tr = 0;
+    if (bad) {
+      te = 3;
+    } else {
+      /* reward / termination (:237-261), float32 arithmetic on the frame */
+      float alt = f[2];
+      if (alt < crash) { r = -10.0; te = 1; }
+      float dx = f[0] - f[12], dy = f[1] - f[13];
+      volatile float d2 = dx * dx;
+      d2 = d2 + dy * dy;
+      float dalt = alt - f[14];
+      if (!te && sqrtf(d2) < dg && fabsf(dalt) < dg) { r = 10.0; te = 1; }
+      tr = e->step >= h->cfg.max_steps; /* env :260 OR gymnasium TimeLimit(1200) */
+      /* PositionReward (:493-507) */
+      float gx = f[12] - f[0], gy = f[13] - f[1], gz = f[14] - f[2];
+      float dcur = norm3f(gx, gy, gz);
+      float ddiff = e->last_d - dcur;
+      r += h->cfg.goal_gain * (double)ddiff;
+      e->last_d = dcur;
+      e->ep_ret += r;                                               /* Monitor :96-99 */
+    }
     rew[i] = (float)r;
     term[i] = (uint8_t)te;
     trunc[i] = (uint8_t)tr;

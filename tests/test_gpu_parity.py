@@ -443,3 +443,40 @@ def test_gymnasium_vector_env_contract(torch_mod):
     assert finished >= 2 * n  # truncation at 7 steps
     env.close()
     sb3.close()
+
+
+def test_nan_guard_quarantines_nonfinite_lanes(torch_mod):
+    """F16_FLAG_NAN_GUARD (failure detection): lanes whose state is poisoned (NaN
+    inertial velocity injected through f16env_set_state) end their next step terminated == 3
+    with reward 0, come back as finite reset rows, and are counted; the other lanes step bit for
+    bit as without the guard. Without the guard the NaN reaches the observation, as it would in
+    the reference (jsbsim_gym.py:268-285 only prints a warning)."""
+    torch = torch_mod
+    from f16_jsb_amd.abi import F16C_VI
+    from f16_jsb_amd.env import F16Envs
+    n = 256
+    a = F16Envs(n, stack_k=4, seed=2, nan_guard=True)
+    b = F16Envs(n, stack_k=4, seed=2)
+    a.reset()
+    b.reset()
+    for t in range(5):
+        act = a.sample_actions(1, t)
+        a.step(act)
+        b.step(act)
+    bad = [3, 77, 200]
+    for h in (a, b):
+        s = h.get_state()
+        s[bad, F16C_VI] = float("nan")
+        h.set_state(s)
+    act = a.sample_actions(1, 99)
+    oa, ob = a.step(act), b.step(act)
+    term = oa.terminated.cpu().numpy()
+    assert list(np.flatnonzero(term == 3)) == bad
+    assert (oa.rew.cpu().numpy()[bad] == 0).all()
+    assert torch.isfinite(oa.obs).all()
+    assert a.nonfinite_count == len(bad) and b.nonfinite_count == 0
+    good = torch.as_tensor(np.setdiff1d(np.arange(n), bad)).cuda()
+    assert torch.equal(oa.obs[good], ob.obs[good]) and torch.equal(oa.rew[good], ob.rew[good])
+    assert not bool(torch.isfinite(ob.obs[bad]).all())
+    a.close()
+    b.close()
