@@ -427,7 +427,7 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
 // frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
 // 160 KB). sT is then unused.
-template <int MODE, bool GT = false, bool ROLL = false>
+template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
@@ -507,7 +507,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       se = sin(L.epa);
     }
     const AltRef A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
-    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
     make_frame(L, ce, se, A, f);                              // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261) in float32, then PositionReward (:493-507)
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(StepArgs a) {
 template <int MODE, int OCC, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
   STEP_SHARED
-  step_body<MODE, false, ROLL>(a, sT, sTmpl, sDone, dynl);
+  step_body<MODE, false, ROLL, OCC == 2>(a, sT, sTmpl, sDone, dynl);
 }
 // global-table variant (large K on the LDS-image path): no LDS table copy
 template <int MODE, bool ROLL = false>
