@@ -200,6 +200,71 @@ def features_bench(envs, stream, iters=200):
             "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5)}
 
 
+def telemetry_bench(envs, stream, iters=200):
+    """SURVEY 8f rank 4 beside the headline: render/telemetry poses (jsbsim_gym.py:381-415) of
+    every env's newest frame, strided read of the (N, K, 15) obs; HBM-bound, 100 B/env."""
+    import torch
+    from f16_jsb_amd.telemetry import poses
+    obs = envs.obs
+    out = torch.empty((obs.shape[0], 10), dtype=torch.float32, device=obs.device)
+    for _ in range(10):
+        poses(obs, out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(iters):
+        poses(obs, out)
+    e.record(stream)
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    n = obs.shape[0]
+    gbps = n * 100 / (ms * 1e-3) / 1e9
+    return {"kernel": "f16_poses_kernel", "envs": n, "ms": round(ms, 5), "envs_per_s": round(n / (ms * 1e-3), 1),
+            "achieved_GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_env": 100}
+
+
+def cfg2_bench(dev, n=4096, steps=1200):
+    """BASELINE cfg2: 4 096 envs on a 64 x 64 altitude x airspeed grid, each trimmed for level
+    flight on the device (f16env_trim), then flown with its constant trim action for 1 200
+    steps (the parity check of this config is tests/test_gpu_parity.py::
+    test_cfg2_trimmed_level_flight_4096). Times the trim and the steps."""
+    import numpy as np
+    import torch
+    from f16_jsb_amd.abi import F16_IC_N
+    from f16_jsb_amd.env import F16Envs
+    e = F16Envs(n, stack_k=4, device=dev, seed=3, max_steps=10**6)
+    ic = np.zeros((n, F16_IC_N))
+    ic[:] = np.array(list(e.cfg.ic))
+    side = int(round(n ** 0.5))
+    hh, uu = np.meshgrid(np.linspace(3000, 30000, side), np.linspace(600, 1200, n // side), indexing="ij")
+    ic[:, 2], ic[:, 3] = hh.ravel()[:n], uu.ravel()[:n]
+    ic_d = torch.as_tensor(ic, device=dev)
+    e.trim(ic_d)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t_ic, res = e.trim(ic_d)
+    torch.cuda.synchronize()
+    trim_s = time.perf_counter() - t0
+    ok = float((res.max(dim=1).values < 1e-2).float().mean())
+    goals = torch.zeros((n, 3), dtype=torch.float32, device=dev)
+    goals[:, 2] = 50000.0
+    e.reset(goals=goals, ic=t_ic)
+    act = torch.zeros((n, 4), dtype=torch.float32, device=dev)
+    act[:, 1], act[:, 3] = t_ic[:, 13].float(), t_ic[:, 15].float()
+    for _ in range(10):
+        e.step(act)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.step(act)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    e.close()
+    return {"workload": "BASELINE cfg2: %d envs, device trim (alpha, elevator, throttle Newton) on a %dx%d "
+                        "altitude x airspeed grid, constant trim action" % (n, side, n // side),
+            "trim_ms": round(trim_s * 1e3, 3), "trimmed_fraction": round(ok, 4), "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 5), "env_steps_per_s": round(n * steps / el, 1)}
+
+
 def sb3_compat_bench(dev, n, steps=20):
     """SURVEY 8d 'also reported': the SB3 drop-in mode -- F16VecEnv with numpy returns and the
     per-env infos list (dummy_vec_env.py:56-73 semantics), at the reference's stack K=10 --
@@ -309,6 +374,7 @@ def main():
     kern_ms, kern_min_ms, _ = envs.profile_kernel(second_pass, nk)
     done_frac = float(((envs.term | envs.trunc).sum()).item()) / n
     feat = features_bench(envs, stream)
+    telem = telemetry_bench(envs, stream)
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step, kern_min_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -317,6 +383,7 @@ def main():
     del acts, warm
     torch.cuda.empty_cache()
     sb3 = sb3_compat_bench(dev, n) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
+    cfg2 = cfg2_bench(dev) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
         rollout = rollout_bench(args, dev, rank, world)
@@ -381,11 +448,14 @@ def main():
         },
         "done_fraction_last_step": round(done_frac, 5),
         "features": feat,
+        "telemetry": telem,
     }
     if rollout is not None:
         out["rollout"] = rollout
     if sb3 is not None:
         out["sb3_compat"] = sb3
+    if cfg2 is not None:
+        out["cfg2"] = cfg2
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
     print(json.dumps(out), flush=True)
