@@ -28,6 +28,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# kernel arguments in device memory (this ROCm's default, pinned here): with them in host memory
+# every step launch pays ~3 us more for its first scalar loads (tools/size_sweep.py A/B)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 METRIC = "env-steps/sec at 65 536 envs, 1/2/4/8 MI355X; HBM GB/s fraction"
 HBM_PEAK_GBPS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
