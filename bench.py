@@ -120,9 +120,15 @@ def rollout_bench(args, dev, rank, world):
             dist.barrier()
         sync()
 
+    # the same rollout as one fused launch per step (f16env_step_rollout), for comparison
+    barrier()
+    tf0 = time.perf_counter()
+    collect_rollout(envs, buf, args.seed + 5000, persistent=False)
+    sync()
+    fused_s = time.perf_counter() - tf0
     barrier()
     t0 = time.perf_counter()
-    last_v, last_d = collect_rollout(envs, buf, args.seed + 4000)
+    last_v, last_d = collect_rollout(envs, buf, args.seed + 4000)  # one persistent launch
     sync()
     t1 = time.perf_counter()
     buf.compute_returns_and_advantage(last_v, last_d)
@@ -141,7 +147,7 @@ def rollout_bench(args, dev, rank, world):
         if rank == 0:
             gathered = sum(v.numel() * v.element_size() for v in out.values())
         del out
-    tt = torch.tensor([t1 - t0, t2 - t1, t_gather], dtype=torch.float64, device=dev)
+    tt = torch.tensor([t1 - t0, t2 - t1, t_gather, fused_s], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     shard_bytes = sum(v.numel() * v.element_size() for v in buf.state_dict().values())
@@ -153,6 +159,9 @@ def rollout_bench(args, dev, rank, world):
                     "Philox; values/log-probs zero: policy network out of scope)" % (n, world, T, args.stack),
         "rollout_s": round(float(tt[0]), 4),
         "rollout_env_steps_per_s": round(n * world * T / float(tt[0]), 1),
+        "rollout_kernel": "f16_rollout_kernel (the whole rollout in one launch, state on-chip)",
+        "rollout_fused_steps_s": round(float(tt[3]), 4),
+        "rollout_fused_steps_env_steps_per_s": round(n * world * T / float(tt[3]), 1),
         "gae_ms": round(float(tt[1]) * 1e3, 3),
         "shard_bytes_per_rank": shard_bytes,
         "gather_s": round(float(tt[2]), 4) if world > 1 else None,

@@ -54,6 +54,7 @@ def lib():
     _set(L, "f16env_step_rollout", [vp, vp, ctypes.POINTER(RolloutSlot)] + [vp] * 11, i32)
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_nonfinite_count.argtypes = [vp, vp, ctypes.POINTER(u64)]
+    L.f16env_rollout_random.argtypes = [vp, vp, u64, u64, i32] + [vp] * 7
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
     L.f16env_sample_actions.argtypes = [vp, vp, u64, u64, vp]
@@ -88,7 +89,7 @@ def check(status: int, what: str):
 # symbols include/f16env.h declares (tests check the .so exports every one of them)
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
-    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count",
+    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_rollout_random",
     "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",

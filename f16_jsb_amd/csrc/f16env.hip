@@ -277,6 +277,41 @@ struct EnvArgs {
   float gust_a, gust_b, gust_sigma;  // cfg5 Gauss-Markov gust coefficients
 };
 
+// reward / termination (jsbsim_gym.py:237-261) in float32, then PositionReward (:493-507), on
+// the new frame f; Monitor's return (monitor.py:96-99). Returns the flags: bit 0 terminated,
+// 1 truncated, 2 quarantined by F16_FLAG_NAN_GUARD (a non-finite position / Mach / alpha /
+// beta / body rate; the angles f[9..11] are already NaN -> 0 by normalize_angle_mpi_pi).
+__device__ __forceinline__ int env_reward(Lane& L, const float* f, const EnvArgs& E, float& r32) {
+  int te = 0, tr;
+  bool bad = false;
+  if (E.flags & F16_FLAG_NAN_GUARD) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) bad = bad || !isfinite(f[j]);
+  }
+  if (bad) {
+    te = 5;  // terminated + quarantined (bit 2), reported as terminated[i] = 3
+    tr = 0;
+    r32 = 0.0f;
+  } else {
+#pragma clang fp contract(off)
+    double r = 0.0;
+    const float alt = f[2];
+    if (alt < E.crash) { r = -10.0; te = 1; }
+    const float dx = f[0] - f[12], dy = f[1] - f[13];
+    float d2 = dx * dx;
+    d2 = d2 + dy * dy;
+    if (!te && sqrtf(d2) < E.dg && fabsf(alt - f[14]) < E.dg) { r = 10.0; te = 1; }
+    tr = L.step >= E.max_steps ? 1 : 0;                   // env :260 | TimeLimit
+    const float dcur = norm3f(f[12] - f[0], f[13] - f[1], f[14] - f[2]);
+    const float ddiff = L.last_d - dcur;
+    r = r + E.gain * (double)ddiff;
+    L.last_d = dcur;
+    L.ep_ret += r;                                         // monitor.py:96-99
+    r32 = (float)r;
+  }
+  return te | (tr << 1);
+}
+
 // reset a lane and produce its frame 0: the IC template copy (default config), or the full
 // RunIC of a per-lane / random / config IC (cfg5 modes: the gust enters the IC passes)
 __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const float* goal,
@@ -341,6 +376,18 @@ __device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl
   f0[12] = L.goal[0]; f0[13] = L.goal[1]; f0[14] = L.goal[2];
 #endif
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
+}
+
+// Earth position angle -> (cos, sin), once per env step (fp64)
+__device__ __forceinline__ void earth_angle(double epa, double& ce, double& se) {
+  if (fabs(epa) < 0.01) {  // series, exact in fp64 for |epa| < 0.01 (40 s episodes: 3e-3)
+    const double e2 = epa * epa;
+    ce = 1.0 - e2 * (0.5 - e2 * (1.0 / 24.0 - e2 * (1.0 / 720.0 - e2 * (1.0 / 40320.0))));
+    se = epa * (1.0 - e2 * (1.0 / 6.0 - e2 * (1.0 / 120.0 - e2 * (1.0 / 5040.0 - e2 * (1.0 / 362880.0)))));
+  } else {
+    ce = cos(epa);
+    se = sin(epa);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -498,53 +545,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       }
     }
     double ce, se;
-    if (fabs(L.epa) < 0.01) {  // series, exact in fp64 for |epa| < 0.01 (40 s episodes: 3e-3)
-      const double e2 = L.epa * L.epa;
-      ce = 1.0 - e2 * (0.5 - e2 * (1.0 / 24.0 - e2 * (1.0 / 720.0 - e2 * (1.0 / 40320.0))));
-      se = L.epa * (1.0 - e2 * (1.0 / 6.0 - e2 * (1.0 / 120.0 - e2 * (1.0 / 5040.0 - e2 * (1.0 / 362880.0)))));
-    } else {
-      ce = cos(L.epa);
-      se = sin(L.epa);
-    }
+    earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
     for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
     make_frame(L, ce, se, A, f);                              // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
-    // reward / termination (:237-261) in float32, then PositionReward (:493-507)
+    // reward / termination (:237-261), PositionReward (:493-507)
     float r32;
-    int te = 0, tr;
-    // F16_FLAG_NAN_GUARD: a non-finite position / Mach / alpha / beta / body rate (the angles
-    // f[9..11] are already NaN -> 0 by normalize_angle_mpi_pi) quarantines the lane
-    bool bad = false;
-    if (a.E.flags & F16_FLAG_NAN_GUARD) {
-#pragma unroll
-      for (int j = 0; j < 9; ++j) bad = bad || !isfinite(f[j]);
-    }
-    if (bad) {
-      te = 5;  // terminated + quarantined (bit 2), reported as terminated[i] = 3
-      tr = 0;
-      r32 = 0.0f;
-    } else {
-#pragma clang fp contract(off)
-      double r = 0.0;
-      const float alt = f[2];
-      if (alt < a.E.crash) { r = -10.0; te = 1; }
-      const float dx = f[0] - f[12], dy = f[1] - f[13];
-      float d2 = dx * dx;
-      d2 = d2 + dy * dy;
-      if (!te && sqrtf(d2) < a.E.dg && fabsf(alt - f[14]) < a.E.dg) { r = 10.0; te = 1; }
-      tr = L.step >= a.E.max_steps ? 1 : 0;                 // env :260 | TimeLimit
-      const float dcur = norm3f(f[12] - f[0], f[13] - f[1], f[14] - f[2]);
-      const float ddiff = L.last_d - dcur;
-      r = r + a.E.gain * (double)ddiff;
-      L.last_d = dcur;
-      L.ep_ret += r;                                         // monitor.py:96-99
-      r32 = (float)r;
-    }
+    flags_out = env_reward(L, f, a.E, r32);  // bit 0 terminated, 1 truncated, 2 quarantined
     F16_STAMP(stamps, ST_REWARD);
-    done = te | tr;
+    done = flags_out & 3;
     rew_out = r32;
-    flags_out = te | (tr << 1);  // bit 0 terminated, 1 truncated, 2 quarantined
   }
   // the stack DMA issued after the prologue has long landed; retire it here, before any
   // store of this step (vmcnt also counts stores on CDNA, so a later wait would drain them)
@@ -788,6 +799,111 @@ static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {
        {f16_step_gt_kernel<0, true>, f16_step_gt_kernel<1, true>, f16_step_gt_kernel<2, true>,
         f16_step_gt_kernel<3, true>}}};
   return table[roll ? 1 : 0][variant < 0 || variant > 2 ? 0 : variant][mode & 3];
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent rollout under the uniform random policy (f16env_rollout_random): T env steps of
+// every lane in ONE launch. The actions come from the f16env_sample_actions Philox stream, so
+// no step waits for a host or a policy: each lane keeps its state in registers and its last K
+// frames in an LDS ring across the whole rollout, and per step writes only the rollout slot
+// (newest frame of the observation acted on, action, reward, next episode start). State and
+// the final observation stack are stored once, at the end. Same arithmetic, RNG streams and
+// auto-reset as T launches of the fused step (f16env_step_rollout): identical actions and
+// episode starts, frames and rewards equal up to fp32 rounding (compiled in another kernel,
+// a few products contract differently).
+// ------------------------------------------------------------------------------------------
+struct RollArgs {
+  SoA s, tmpl;
+  const float* obs_prev;  // N x K x 15 before step 0
+  float* obs;             // N x K x 15 after step T-1
+  float* frames;          // T x N x 15
+  float* actions;         // T x N x 4
+  float* rewards;         // T x N
+  float* next_start;      // (T - 1) x N: 1.0 where the lane finished at step t < T-1
+  float* last_start;      // N: the same for step T-1
+  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine count
+  uint64_t seed, step0;
+  int32_t T;
+  EnvArgs E;
+  ModelConsts C;
+};
+static constexpr int RING_PITCH = 16;  // floats per ring frame slot (15 used)
+__global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
+  __shared__ __align__(16) float4 sTmpl[NCOL + TMPL_FRAME_COLS];
+  extern __shared__ __align__(16) float ring[];  // [K][BLOCK][RING_PITCH]
+  const int K = a.E.K, tid = threadIdx.x;
+  const int64_t k = (int64_t)blockIdx.x * BLOCK + tid;
+  const bool live = k < a.E.n;
+  stage_tables_issue(sT);
+  if (tid < NCOL + TMPL_FRAME_COLS)
+    dma16(reinterpret_cast<const float*>(a.tmpl.c + (tid < NCOL ? tid : tid + NCOL_ALL - NCOL)),
+          reinterpret_cast<float*>(sTmpl));
+  Lane L;
+  if (live) lane_load(a.s, k, L);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!live) return;  // no barrier below
+  float* my = ring + (size_t)tid * RING_PITCH;
+  const size_t slot_stride = (size_t)BLOCK * RING_PITCH;
+  {
+    const float* op = a.obs_prev + k * (int64_t)K * F16_OBS_DIM;
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = op[j * F16_OBS_DIM + c];
+  }
+  float prevf[F16_OBS_DIM];  // newest frame of the observation the next action acts on
+#pragma unroll
+  for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = my[(K - 1) * slot_stride + c];
+  int head = 0;  // ring slot of the oldest frame
+  const int64_t N = a.E.n;
+  const uint64_t gid = (uint64_t)(a.E.id_base + k);
+  for (int t = 0; t < a.T; ++t) {
+    const float4 av = philox_action(a.seed, gid, a.step0 + (uint64_t)t);
+    const float cmd[4] = {av.x, av.y, av.z, av.w};
+    L.step += 1;                                              // jsbsim_gym.py:215
+    double ce, se;
+    earth_angle(L.epa, ce, se);
+    const AltRef A = alt_ref(L, ce, se);
+    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, A, sT, a.C, false);  // :225-232
+    float f[F16_OBS_DIM];
+    make_frame(L, ce, se, A, f);                              // :234
+    float r32;
+    const int fl = env_reward(L, f, a.E, r32);
+    const int done = fl & 3;
+    if (fl & 4) atomicAdd(a.nonfinite, 1ull);  // rare: one lane at a time
+    const int64_t row = (int64_t)t * N + k;
+    float* fr = a.frames + row * F16_OBS_DIM;
+#pragma unroll
+    for (int c = 0; c < F16_OBS_DIM; ++c) fr[c] = prevf[c];
+    reinterpret_cast<float4*>(a.actions)[row] = av;
+    a.rewards[row] = r32;
+    if (t + 1 < a.T) a.next_start[row] = done ? 1.0f : 0.0f;
+    else a.last_start[k] = done ? 1.0f : 0.0f;
+    if (done) {  // dummy_vec_env.py:68-71: the next observation is K x the reset frame
+      float f0[F16_OBS_DIM];
+      lane_reset_template(L, sTmpl, a.E, k, f0);
+      for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = f0[c];
+      head = 0;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = f0[c];
+    } else {  // deque append (:235): the oldest frame's slot takes the new one
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) my[head * slot_stride + c] = f[c];
+      head = (head + 1 == K) ? 0 : head + 1;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = f[c];
+    }
+  }
+  lane_store(a.s, k, L);
+  float* o = a.obs + k * (int64_t)K * F16_OBS_DIM;
+  for (int j = 0; j < K; ++j) {
+    const int sl = (head + j) % K;
+#pragma unroll
+    for (int c = 0; c < F16_OBS_DIM; ++c) o[j * F16_OBS_DIM + c] = my[sl * slot_stride + c];
+  }
 }
 
 // cfg5 auto-reset of the lanes a deferred-mode step finished (done list from its ballot
@@ -1336,6 +1452,10 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
       }
     }
   }
+  if (cfg->stack_k <= 8 &&
+      hipFuncSetAttribute((const void*)f16_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(sizeof(float) * cfg->stack_k * BLOCK * RING_PITCH)) != hipSuccess)
+    (void)hipGetLastError();  // f16env_rollout_random reports it
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + F16_IC_N, cfg->ic_lo, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + 2 * F16_IC_N, cfg->ic_hi, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
@@ -1492,6 +1612,29 @@ int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count) {
   HIPCHK(hipMemcpyAsync(&v, h->nonfinite, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   *count = (uint64_t)v;
+  return 0;
+}
+
+int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T, const float* obs_prev,
+                          float* obs, float* frames, float* actions, float* rewards, float* next_start,
+                          float* last_start) {
+  if (!h) return set_err(-1, "null handle");
+  if (T < 1) return set_err(-1, "T must be >= 1");
+  if (!obs_prev || !obs || !frames || !actions || !rewards || !last_start || (T > 1 && !next_start))
+    return set_err(-1, "obs_prev/obs/frames/actions/rewards/last_start (and next_start for T > 1) are required");
+  if (((uintptr_t)actions & 15) != 0) return set_err(-1, "actions must be 16-byte aligned");
+  if (h->mode != 0 || (h->cfg.flags & F16_FLAG_NO_AUTORESET))
+    return set_err(-1, "rollout_random needs the reference task (no cfg5 modes) with auto-reset");
+  if (h->cfg.stack_k > 8) return set_err(-1, "rollout_random keeps the stack in LDS: stack_k <= 8");
+  RollArgs a;
+  a.s = h->soa; a.tmpl = h->tmpl; a.obs_prev = obs_prev; a.obs = obs; a.frames = frames; a.actions = actions;
+  a.rewards = rewards; a.next_start = next_start; a.last_start = last_start; a.nonfinite = h->nonfinite;
+  a.seed = seed; a.step0 = step0; a.T = T;
+  a.E = env_args(h);
+  a.C = h->C;
+  const size_t ring = sizeof(float) * h->cfg.stack_k * BLOCK * RING_PITCH;
+  hipLaunchKernelGGL(f16_rollout_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), ring, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 

@@ -193,6 +193,30 @@ class F16Envs:
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
+    def rollout_random(self, seed: int, step0: int, n_steps: int, frames, actions, rewards, next_start,
+                       last_start) -> None:
+        """n_steps env steps in ONE launch under the uniform random policy (f16env_rollout_random:
+        actions from the sample_actions(seed, step0 + t) stream, state kept on-chip): writes the
+        rollout slots frames (T, N, 15), actions (T, N, 4), rewards (T, N), next_start (T-1, N)
+        (episode starts of slots 1..T-1) and last_start (N,), and leaves the env at its
+        observation after the last step (self.obs). The same actions and episode starts as n_steps
+        step_rollout calls; frames and rewards equal up to fp32 rounding."""
+        T = int(n_steps)
+        n = self.n
+        for name, x, shape in (("frames", frames, (T, n, F16_OBS_DIM)), ("actions", actions, (T, n, 4)),
+                               ("rewards", rewards, (T, n)), ("last_start", last_start, (n,))):
+            if tuple(x.shape) != shape or x.dtype != self.torch.float32 or not x.is_contiguous():
+                raise ValueError("%s must be a contiguous float32 %s tensor" % (name, shape))
+        if T > 1 and (next_start is None or tuple(next_start.shape) != (T - 1, n) or not next_start.is_contiguous()):
+            raise ValueError("next_start must be a contiguous float32 (T-1, N) tensor")
+        prev = self._obs[self._cur]
+        nxt = self._obs[self._cur ^ 1]
+        check(lib().f16env_rollout_random(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                          int(step0) & 0xFFFFFFFFFFFFFFFF, T, _ptr(prev), _ptr(nxt), _ptr(frames),
+                                          _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(last_start)),
+              "f16env_rollout_random")
+        self._cur ^= 1
+
     def profile_kernel(self, fn, launches: int):
         """Run fn() (which issues `launches` steps) with the step kernel's own dispatch events
         recording each launch; returns (avg_ms, min_ms, launches timed)."""

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 
 import torch
 
-from .abi import F16_OBS_DIM
+from .abi import F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC, F16_OBS_DIM
 
 FIELDS = ("frames", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns")
 
@@ -87,7 +87,8 @@ class DeviceRolloutBuffer:
         return {f: getattr(self, f) for f in FIELDS} | {"obs0": self.obs0}
 
 
-def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None, fused: bool = True):
+def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None, fused: bool = True,
+                    persistent: bool = True):
     """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors with random
     policy actions from the device Philox stream (the policy network is out of scope; values
     and log-probs are zeros unless ``values_fn(obs) -> (values, log_probs)`` is given).
@@ -95,7 +96,10 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, v
 
     fused: each step is ONE launch (f16env_step_rollout) that draws the actions in-kernel and
     writes the slot's frame / actions / rewards / next episode starts itself, instead of a
-    sampling launch, the step and six buffer copies (RolloutBuffer.add, buffers.py:440-479)."""
+    sampling launch, the step and six buffer copies (RolloutBuffer.add, buffers.py:440-479).
+    persistent (with no values_fn, the reference task and K <= 8): the whole rollout is ONE
+    launch (f16env_rollout_random) that keeps every env's state on-chip across the steps: the
+    same actions and episode starts, frames / rewards equal up to fp32 rounding."""
     dev = buf.device
     n = buf.n_envs
     zeros = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -106,7 +110,20 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, v
     buf.reset()
     use_fused = fused and hasattr(envs, "step_rollout") and buf.frames[0].data_ptr() % 16 == 0 \
         and (n * F16_OBS_DIM * 4) % 16 == 0
-    if use_fused:
+    use_persistent = (use_fused and persistent and values_fn is None and hasattr(envs, "rollout_random")
+                      and envs.k <= 8 and not (envs.cfg.flags & (F16_FLAG_NO_AUTORESET | F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS))
+                      and buf.actions.data_ptr() % 16 == 0)
+    if use_persistent:
+        carry = torch.empty(n, dtype=torch.float32, device=dev)
+        buf.obs0.copy_(obs)
+        buf.episode_starts[0].copy_(starts)
+        T = buf.n_steps
+        envs.rollout_random(seed, step0, T, buf.frames, buf.actions, buf.rewards,
+                            buf.episode_starts[1:] if T > 1 else None, carry)
+        obs = envs.obs
+        buf.pos = T
+        starts = carry
+    elif use_fused:
         carry = torch.empty(n, dtype=torch.float32, device=dev)
         buf.obs0.copy_(obs)
         buf.episode_starts[0].copy_(starts)

@@ -220,6 +220,23 @@ int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slo
                         float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx,
                         int32_t* n_done);
 
+/* T env steps of every lane in ONE launch under the uniform random policy (the actions are the
+ * f16env_sample_actions stream (seed; env id, step0 + t)): SURVEY.md 8f rank 1's rollout with
+ * the policy network out of scope. The state stays in registers and the last K frames in LDS
+ * for the whole rollout; per step only the rollout slot is written:
+ *   frames     T x N x 15  newest frame of the observation acted on at step t
+ *   actions    T x N x 4   rewards T x N
+ *   next_start (T-1) x N   1.0 where the lane finished at step t (episode_starts of slot t+1)
+ *   last_start N           the same for step T-1
+ * obs_prev / obs: N x K x 15 before step 0 / after step T-1 (may alias). The same actions and
+ * episode starts as T calls of f16env_step_rollout(seed, step0 + t, ...), frames and rewards
+ * equal up to fp32 rounding (the same arithmetic compiled in another kernel). Reference task
+ * only (no cfg5 modes, auto-reset on), stack_k <= 8. Replaces on_policy_algorithm.py:194-262's
+ * loop for that policy. */
+int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T,
+                          const float* obs_prev, float* obs, float* frames, float* actions,
+                          float* rewards, float* next_start, float* last_start);
+
 /* Lanes quarantined by F16_FLAG_NAN_GUARD since create (waits for `stream`). */
 int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);
 
