@@ -234,6 +234,36 @@ def telemetry_bench(envs, stream, iters=200):
             "achieved_GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_env": 100}
 
 
+def persistent_bench(dev, n, stack, steps, seed):
+    """The headline workload (n envs, stack K, random actions, auto-reset) run as ONE
+    persistent launch (f16env_rollout_random: actions drawn in-kernel from the same Philox
+    stream, state on-chip, per step only the rollout slot written) -- what a step costs without
+    the per-step launch, prologue and state traffic. Not the headline: the headline steps
+    through the VecEnv boundary with the actions handed in each step."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    e = F16Envs(n, stack_k=stack, device=dev, seed=seed)
+    e.reset()
+    f32 = torch.float32
+    fr = torch.empty((steps, n, 15), dtype=f32, device=dev)
+    ac = torch.empty((steps, n, 4), dtype=f32, device=dev)
+    rw = torch.empty((steps, n), dtype=f32, device=dev)
+    ns = torch.empty((steps - 1, n), dtype=f32, device=dev)
+    ls = torch.empty(n, dtype=f32, device=dev)
+    e.rollout_random(seed, 0, 20, fr[:20], ac[:20], rw[:20], ns[:19], ls)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.rollout_random(seed, 20, steps, fr, ac, rw, ns, ls)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    e.close()
+    del fr, ac, rw, ns
+    torch.cuda.empty_cache()
+    return {"kernel": "f16_rollout_kernel", "envs": n, "stack_k": stack, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 5), "env_steps_per_s": round(n * steps / el, 1),
+            "note": "one launch for all steps, actions drawn in-kernel (random policy); not the headline"}
+
+
 def cfg2_bench(dev, n=4096, steps=1200):
     """BASELINE cfg2: 4 096 envs on a 64 x 64 altitude x airspeed grid, each trimmed for level
     flight on the device (f16env_trim), then flown with its constant trim action for 1 200
@@ -396,6 +426,7 @@ def main():
     torch.cuda.empty_cache()
     sb3 = sb3_compat_bench(dev, n) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
     cfg2 = cfg2_bench(dev) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
+    persist = persistent_bench(dev, n, args.stack, 1000, args.seed + 6000) if (world == 1 and not cfg5) else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
         rollout = rollout_bench(args, dev, rank, world)
@@ -468,6 +499,8 @@ def main():
         out["sb3_compat"] = sb3
     if cfg2 is not None:
         out["cfg2"] = cfg2
+    if persist is not None:
+        out["persistent_random_policy"] = persist
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
     print(json.dumps(out), flush=True)
