@@ -346,6 +346,23 @@ def load_traffic(envs, stack, state_bytes):
     return None
 
 
+def load_valu(envs, stack):
+    """VALU side of the step kernel (SURVEY 8(d) asks for it beside the HBM fraction): the
+    committed SQ-counter summary (tools/pmc_valu.py), if it was measured on this workload.
+    The VALU issue peak for one wave per SIMD is one wave64 instruction per 4 cycles."""
+    p = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("envs") == envs and d.get("stack_k") == stack:
+            return {"valu_insts_per_wave_step": d["valu_insts_per_wave_step"], "valu_busy_frac": d["valu_busy_frac"],
+                    "wait_any_frac": d["wait_any_frac"], "wave_cycles": d["wave_cycles"],
+                    "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_* passes)"}
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -477,6 +494,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
+            "valu": None if cfg5 else load_valu(n, args.stack),
             "kernel": kernel_name + (" + f16_reset_done_kernel" if cfg5 else ""),
             "waves_per_simd": waves_per_simd,
             "kernel_ms": round(roof_ms, 5),

@@ -42,7 +42,7 @@ for s in $STEPS; do
     prof)
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \
         python bench.py --steps 300 --warmup 20 --no-cpu-baseline --rollout-envs 0 ;;
-    sq)
+    sq)  # summary: python tools/pmc_valu.py gpurun_out/pmc_sq*_$TAG --out profiles/pmc_valu.json
       run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_sq_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- \
