@@ -93,7 +93,14 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
     cfg1 = {"value": round(1000 / el1, 1), "unit": "env-steps/s", "cores": 1,
             "sample": "BASELINE cfg1: 1 env x 1000 random-action steps (numpy default_rng(0), K=10), "
                       "oracle/f16ref.c through its ctypes step (one env, no parallelism)"}
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port", "cfg1": cfg1,
+            "host": {"cpu_model": model, "os_cpu_count": os.cpu_count()},
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
                       "%d envs x %d random-action steps (stack=%d, auto-reset%s), %d OpenMP threads, %.1f s"
                       % (n, steps, stack, ", cfg5 random IC + gusts" if cfg5 else "", threads, el)}
