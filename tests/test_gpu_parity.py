@@ -177,6 +177,54 @@ def test_autoreset_crash_parity(torch_mod):
     assert saw.all()
 
 
+def test_autoreset_goal_reached_parity(torch_mod):
+    """Goal reached (jsbsim_gym.py:248-255: horizontal distance < dg = 100 m and |h - gz| <
+    100 m -> +10, terminated) at staggered steps, then auto-reset: done flags and episode
+    lengths bit-exact, rewards / returns / terminal obs within the step tolerances. Goals
+    are placed along the IC heading (north, frame x = lat*R), one group out of reach by
+    altitude (never terminates)."""
+    torch = torch_mod
+    n = 64
+    act1 = np.array([[0.0, 0.0, 0.0, 0.6]], np.float32)
+    # the flight path does not depend on the goal: probe it once, then put env i's goal so
+    # that it comes within 100 m half-way between steps i and i+1 (~4.5 m from either side
+    # of the threshold, far beyond the fp32 position error)
+    probe = OracleEnvs(1, stack_k=4, seed=91)
+    probe.reset(goals=np.array([[0.0, 0.0, 9000.0]], np.float32), ic=default_ic()[None])
+    xs = [0.0] + [float(probe.step(act1)[0][0, -1, 0]) for _ in range(50)]
+    probe.close()
+    ic = np.tile(default_ic(), (n, 1))
+    goals = np.zeros((n, 3), np.float32)
+    y = np.linspace(-60.0, 60.0, 48)
+    goals[:48, 1] = y
+    goals[:48, 0] = [0.5 * (xs[i] + xs[i + 1]) + np.sqrt(1e4 - y[i] ** 2) for i in range(48)]
+    goals[:, 2] = 1524.0
+    goals[48:, 0] = np.linspace(30.0, 600.0, 16)
+    goals[48:, 2] = 1524.0 + 400.0                 # out of reach in altitude
+    ref, g = _pair(n, 4, seed=91)
+    ref.reset(goals=goals, ic=ic)
+    g.reset(goals=goals, ic=ic)
+    act = np.tile(act1, (n, 1))
+    ta = torch.as_tensor(act).cuda()
+    first = np.zeros(n, bool)
+    for t in range(60):
+        o_r, r_r, te_r, tr_r, tobs_r, eret_r, elen_r = ref.step(act)
+        out = g.step(ta)
+        te_g = out.terminated.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(te_g, te_r, err_msg="terminated @%d" % t)
+        np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3, err_msg="reward @%d" % t)
+        d = te_r & ~first  # each env's first episode end (later ones start from a Philox goal)
+        if d.any():
+            assert (r_r[d] > 9.0).all()  # the +10 goal reward, not the -10 crash
+            np.testing.assert_allclose(out.ep_return.cpu().numpy()[d], eret_r[d], atol=1e-3)
+            np.testing.assert_array_equal(out.ep_len.cpu().numpy()[d], elen_r[d])
+            _assert_frames(out.terminal_obs.cpu().numpy()[d, -1], tobs_r[d, -1], TOL_CONST300, "terminal obs")
+            first |= d
+            if t < 48:
+                assert d[t]  # env t reaches its goal at step t + 1
+    assert first[:48].all() and not first[48:].any()
+
+
 def test_autoreset_frame_equals_reset_kernel_frame(torch_mod):
     """The step kernel's auto-reset copies frame 0 of the IC template, evaluated once at create
     (f16_ic_kernel); f16env_reset evaluates it per lane (f16_reset_kernel). For the same IC
