@@ -131,6 +131,8 @@ class F16Envs:
         m = None if mask is None else t.as_tensor(mask, device=self.device).to(t.uint8).contiguous()
         g = None if goals is None else t.as_tensor(goals, device=self.device, dtype=t.float32).contiguous()
         c = None if ic is None else t.as_tensor(ic, device=self.device, dtype=t.float64).contiguous()
+        if m is not None and tuple(m.shape) != (self.n,):
+            raise ValueError("mask must be (N,), got %s" % (tuple(m.shape),))
         if g is not None and tuple(g.shape) != (self.n, 3):
             raise ValueError("goals must be (N, 3)")
         if c is not None and tuple(c.shape) != (self.n, F16_IC_N):
@@ -138,6 +140,16 @@ class F16Envs:
         out = self._obs[self._cur]
         check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
         return out
+
+    def _need(self, x, shape, dtype, name):
+        """Host-side check of a caller buffer the kernel indexes by env: a wrong shape would be
+        an out-of-bounds access on the device, so it is refused before the launch."""
+        t = self.torch
+        if x is None:
+            return
+        if not isinstance(x, t.Tensor) or x.device != self.device or x.dtype != dtype or not x.is_contiguous() \
+                or tuple(x.shape) != tuple(shape):
+            raise ValueError("%s must be a contiguous %s %s tensor on %s" % (name, dtype, tuple(shape), self.device))
 
     def step(self, actions, done_idx=None, n_done=None, features=None) -> StepOut:
         """One env step for all lanes; ``actions`` (N,4) float32 device tensor (or host
@@ -156,6 +168,10 @@ class F16Envs:
             act = self._act
         if tuple(act.shape) != (self.n, 4):
             raise ValueError("actions must be (N, 4), got %s" % (tuple(act.shape),))
+        if (done_idx is None) != (n_done is None):
+            raise ValueError("done_idx and n_done go together")
+        self._need(done_idx, (self.n,), t.int32, "done_idx")
+        self._need(n_done, (1,), t.int32, "n_done")
         prev = self._obs[self._cur]
         nxt = self._obs[self._cur ^ 1]
         check(lib().f16env_step(self._h, self._stream(), _ptr(act), _ptr(prev), _ptr(nxt), _ptr(self.rew),
@@ -180,6 +196,12 @@ class F16Envs:
             else:
                 self._act.copy_(t.as_tensor(policy_actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
                 act = self._act
+            if tuple(act.shape) != (self.n, 4):
+                raise ValueError("policy_actions must be (N, 4), got %s" % (tuple(act.shape),))
+        self._need(frame, (self.n, F16_OBS_DIM), t.float32, "frame")
+        self._need(actions, (self.n, 4), t.float32, "actions")
+        self._need(rewards, (self.n,), t.float32, "rewards")
+        self._need(next_start, (self.n,), t.float32, "next_start")
         if features is not None and (tuple(features.shape) != (self.n, self.k, 17) or features.dtype != t.float32
                                      or not features.is_contiguous()):
             raise ValueError("features must be a contiguous float32 (N, K, 17) tensor")

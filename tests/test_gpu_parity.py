@@ -528,3 +528,31 @@ def test_nan_guard_quarantines_nonfinite_lanes(torch_mod):
     assert not bool(torch.isfinite(ob.obs[bad]).all())
     a.close()
     b.close()
+
+
+def test_host_checks_refuse_misshaped_buffers(torch_mod):
+    """Buffers the kernels index by env are shape-checked on the host before any launch (a
+    wrong size would be an out-of-bounds device access), and the handle stays usable."""
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    n = 70
+    g = F16Envs(n, stack_k=4, seed=2)
+    g.reset()
+    a = g.sample_actions(1, 0)
+    i32 = dict(dtype=torch.int32, device="cuda")
+    f32 = dict(dtype=torch.float32, device="cuda")
+    with pytest.raises(ValueError):
+        g.reset(mask=torch.ones(n - 1, dtype=torch.bool, device="cuda"))
+    with pytest.raises(ValueError):
+        g.step(a[:-1])
+    with pytest.raises(ValueError):
+        g.step(a, done_idx=torch.zeros(n - 6, **i32), n_done=torch.zeros(1, **i32))
+    with pytest.raises(ValueError):
+        g.step(a, done_idx=torch.zeros(n, **i32))
+    with pytest.raises(ValueError):
+        g.step_rollout(1, 0, frame=torch.zeros(n, 14, **f32))
+    with pytest.raises(ValueError):
+        g.step_rollout(1, 0, rewards=torch.zeros(n, dtype=torch.float64, device="cuda"))
+    out = g.step(a, done_idx=torch.zeros(n, **i32), n_done=torch.zeros(1, **i32))
+    assert torch.isfinite(out.obs).all()
+    g.close()
