@@ -71,8 +71,11 @@ class DeviceRolloutBuffer:
 
         if self.device.type != "cuda":
             raise RuntimeError("GAE runs on the GPU (f16env_gae); buffer is on %s" % self.device)
-        lv = last_values.reshape(-1).to(torch.float32).contiguous()
-        dn = dones.reshape(-1).to(torch.uint8).contiguous()
+        lv = torch.as_tensor(last_values).reshape(-1).to(self.device, torch.float32).contiguous()
+        dn = torch.as_tensor(dones).reshape(-1).to(self.device, torch.uint8).contiguous()
+        if lv.numel() != self.n_envs or dn.numel() != self.n_envs:  # the kernel reads n_envs of each
+            raise ValueError("last_values and dones must hold n_envs = %d entries, got %d and %d"
+                             % (self.n_envs, lv.numel(), dn.numel()))
         s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         check(lib().f16env_gae(ctypes.c_void_p(s), self.n_steps, self.n_envs, self.rewards.data_ptr(),
                                self.values.data_ptr(), self.episode_starts.data_ptr(), lv.data_ptr(),
