@@ -80,6 +80,20 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
         if el >= seconds or steps >= 2000:
             break
     e.close()
+    # SURVEY 8(d) also asks for the all-cores rate at N = 4096 (cfg2's env count): 3 s sample
+    n4 = None
+    if n > 4096:
+        e4 = OracleEnvs(4096, stack_k=stack, seed=1, cfg5=cfg5)
+        e4.reset()
+        s4 = 0
+        t4 = time.perf_counter()
+        while time.perf_counter() - t4 < min(3.0, seconds):
+            e4.step(e4.sample_actions(1, s4))
+            s4 += 1
+        el4 = time.perf_counter() - t4
+        e4.close()
+        n4 = {"value": round(4096 * s4 / el4, 1), "unit": "env-steps/s", "cores": threads,
+              "sample": "4096 envs x %d random-action steps, %.1f s" % (s4, el4)}
     # BASELINE cfg1 semantics beside it: ONE env, 1000 random-action steps, reference stack K=10
     e1 = OracleEnvs(1, stack_k=10, seed=1)
     e1.reset()
@@ -100,6 +114,7 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
     except OSError:
         pass
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port", "cfg1": cfg1,
+            "n4096": n4,
             "host": {"cpu_model": model, "os_cpu_count": os.cpu_count()},
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
                       "%d envs x %d random-action steps (stack=%d, auto-reset%s), %d OpenMP threads, %.1f s"
