@@ -37,10 +37,14 @@ def classify(op: str) -> str:
 
 
 def main():
+    # -D/-f flags and -mllvm=OPTION (passed to hipcc as "-mllvm OPTION") go to the compiler
     flags = [a for a in sys.argv[1:] if a.startswith(("-D", "-f"))]
+    for a in sys.argv[1:]:
+        if a.startswith("-mllvm="):
+            flags += ["-mllvm", a[len("-mllvm="):]]
     kernel = "_Z15f16_step_kernel8StepArgs"
     dump = None
-    args = [a for a in sys.argv[1:] if not a.startswith(("-D", "-f"))]
+    args = [a for a in sys.argv[1:] if not a.startswith(("-D", "-f", "-mllvm="))]
     for i, a in enumerate(args):
         if a == "--kernel":
             kernel = args[i + 1]
