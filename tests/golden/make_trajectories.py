@@ -2,9 +2,9 @@
 (oracle/f16ref.c, the fp64 restatement of the JSBSim F-16 path; JSBSim itself is unavailable,
 SURVEY.md 8c), committed so that
 
-  * tests/test_oracle_golden.py pins the oracle against drift (bit-exact re-run on CPU), and
-  * tests/test_gpu_parity.py checks the HIP path against the committed outputs without running
-    the oracle (the tolerances of that file).
+  * tests/test_golden_trajectories.py pins the oracle against drift (bit-exact re-run on CPU),
+    and checks the HIP path against the committed outputs without running the oracle (the
+    tolerances of tests/test_gpu_parity.py).
 
 Two cases, inputs stored beside the outputs:
   const   16 envs, K = 4, altitude 3 000-30 000 ft x airspeed 600-1 200 fps ICs, fixed goals,
