@@ -82,10 +82,18 @@ class F16Envs:
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
         self._act = torch.zeros((n, 4), dtype=f32, device=dev)
+        # the handle's own buffers never move: their addresses are taken once, not per step
+        self._obs_ptr = [o.data_ptr() for o in self._obs]
+        self._out_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
+                         self.terminal_obs.data_ptr(), self.ep_return.data_ptr(), self.ep_len.data_ptr())
+        self._step_fn = L.f16env_step
 
     # --------------------------------------------------------------------------------------
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _stream_int(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
 
     @property
     def obs(self):
@@ -160,6 +168,16 @@ class F16Envs:
         if features is not None:
             return self.step_rollout(0, 0, features=features, policy_actions=actions)
         t = self.torch
+        if done_idx is None and n_done is None and isinstance(actions, t.Tensor) and actions.device == self.device \
+                and actions.dtype == t.float32 and actions.is_contiguous() and actions.shape == (self.n, 4):
+            ap = actions.data_ptr()
+            if ap % 16 == 0:  # the common case: one ctypes call on cached addresses
+                cur = self._cur
+                check(self._step_fn(self._h, self._stream_int(), ap, self._obs_ptr[cur], self._obs_ptr[cur ^ 1],
+                                    *self._out_ptr, None, None), "f16env_step")
+                self._cur = cur ^ 1
+                return StepOut(self._obs[cur ^ 1], self.rew, self.term, self.trunc, self.terminal_obs,
+                               self.ep_return, self.ep_len)
         if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
                 and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
             act = actions
