@@ -287,7 +287,7 @@ def test_trim_parity_and_level_flight(torch_mod):
 
 
 @pytest.mark.parametrize("n,k,steps", [(65536, 4, 200), (4171, 2, 40), (2113, 10, 40), (1000, 8, 40), (777, 3, 40),
-                                       (65, 1, 40), (300, 11, 40)])
+                                       (65, 1, 40), (300, 11, 40), (1, 4, 40), (63, 10, 40)])
 def test_large_batch_properties(torch_mod, n, k, steps):
     """65 536 envs (BASELINE cfg3 shape), 200 random-action steps: finite outputs, the
     ordered-stack invariant obs[t][:, :-1] == obs[t-1][:, 1:] on continuing lanes
