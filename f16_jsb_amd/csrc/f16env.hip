@@ -953,8 +953,11 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   Lane L;
   lane_load<true>(a.s, k, L);
   float f0[F16_OBS_DIM];
-  lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, a.goals ? a.goals + 3 * k : nullptr,
-             a.E, k, sT, a.C, f0);
+  // a goal row whose x is NaN draws the lane's goal from the device stream (mixed seeded /
+  // unseeded resets in ONE call: the episode counter advances once per reset)
+  const float* g = a.goals ? a.goals + 3 * k : nullptr;
+  if (g && isnan(g[0])) g = nullptr;
+  lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, g, a.E, k, sT, a.C, f0);
   lane_store<true>(a.s, k, L);
   if (a.obs) {
     float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;

@@ -75,9 +75,13 @@ class F16Envs:
         n, k = self.n, self.k
         self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
         self._cur = 0
-        self.rew = torch.zeros(n, dtype=f32, device=dev)
-        self.term = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
+        # rewards (f32), terminated, truncated (u8) in ONE allocation, so a host-side consumer
+        # (F16VecEnv's numpy mode) moves the three with a single device-to-host copy
+        nb = (4 * n + 2 * n + 15) // 16 * 16
+        self.step_flags = torch.zeros(nb, dtype=torch.uint8, device=dev)
+        self.rew = self.step_flags[:4 * n].view(f32)
+        self.term = self.step_flags[4 * n:5 * n]
+        self.trunc = self.step_flags[5 * n:6 * n]
         self.terminal_obs = torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev)
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -307,82 +311,186 @@ class F16Envs:
         return out
 
 
-class F16VecEnv:
+def _optional_class(module: str, name: str):
+    """A base class from an optional dependency (stable_baselines3 / gymnasium), or None."""
+    try:
+        mod = __import__(module, fromlist=[name])
+        return getattr(mod, name)
+    except Exception:  # noqa: BLE001 - absent or broken: the duck-typed surface is used
+        return None
+
+
+# stable_baselines3/common/base_class.py:215 accepts an env as-is only when
+# isinstance(env, VecEnv); gymnasium learners check gymnasium.Env / gymnasium.vector.VectorEnv.
+# When those libraries are importable the facades below ARE subclasses of their ABCs.
+SB3VecEnv = _optional_class("stable_baselines3.common.vec_env.base_vec_env", "VecEnv")
+GymEnv = _optional_class("gymnasium", "Env")
+GymVectorEnv = _optional_class("gymnasium.vector", "VectorEnv")
+
+
+def _bases(*classes):
+    return tuple(c for c in classes if c is not None) or (object,)
+
+
+class _ReadOnlyInfo(dict):
+    """The info dict of every lane that did not finish its step: {"TimeLimit.truncated": False}
+    (dummy_vec_env.py:56-73 through TimeLimit + Monitor). ONE shared, immutable instance per
+    step instead of N fresh dicts; lanes that finished get fresh dicts of their own."""
+
+    def _ro(self, *a, **k):
+        raise TypeError("info of a lane that did not finish is shared and read-only")
+
+    __setitem__ = __delitem__ = update = pop = popitem = clear = setdefault = _ro  # type: ignore[assignment]
+
+    def copy(self):
+        return dict(self)
+
+    def __deepcopy__(self, memo):
+        return dict(self)
+
+
+_NOT_DONE_INFO = _ReadOnlyInfo({"TimeLimit.truncated": False})
+
+
+class _HostStaging:
+    """Numpy mode of the facades: pinned host buffers the step's outputs land in, with one
+    stream sync per step. obs goes to a ring of `ring` pinned (N, K, 15) buffers -- the arrays a
+    step returns stay valid for `ring` - 1 further steps (SB3 copies obs into its buffers one step
+    later: on_policy_algorithm.py:250-257, off_policy_algorithm.py _store_transition); rewards /
+    terminated / truncated arrive by ONE copy of the handle's packed step_flags buffer."""
+
+    def __init__(self, envs: "F16Envs", ring: int = 3):
+        t = envs.torch
+        self.t, self.envs = t, envs
+        pin = envs.device.type == "cuda"
+        n, k = envs.n, envs.k
+        self.obs = [t.empty((n, k, F16_OBS_DIM), dtype=t.float32, pin_memory=pin) for _ in range(ring)]
+        self.flags = t.empty(envs.step_flags.shape, dtype=t.uint8, pin_memory=pin)
+        self.act = t.empty((n, 4), dtype=t.float32, pin_memory=pin)
+        self.i = 0
+
+    def actions_to_device(self, actions):
+        """Host actions -> the handle's device action buffer through pinned staging; device
+        float32 (N, 4) tensors pass through untouched."""
+        t, e = self.t, self.envs
+        if isinstance(actions, t.Tensor):
+            if actions.device == e.device and actions.dtype == t.float32 and actions.is_contiguous() \
+                    and tuple(actions.shape) == (e.n, 4):
+                return actions
+            actions = actions.detach().to("cpu", t.float32).numpy()
+        a = np.asarray(actions, dtype=np.float32)
+        if a.size != e.n * 4:
+            raise ValueError("actions must hold (N, 4) = (%d, 4) values, got shape %s" % (e.n, a.shape))
+        self.act.numpy()[...] = a.reshape(e.n, 4)
+        e._act.copy_(self.act, non_blocking=True)
+        return e._act
+
+    def fetch(self, obs_dev, with_flags: bool = True):
+        """Copy obs (and rew/term/trunc) to pinned memory, wait once; numpy views."""
+        o = self.obs[self.i]
+        self.i = (self.i + 1) % len(self.obs)
+        o.copy_(obs_dev, non_blocking=True)
+        if with_flags:
+            self.flags.copy_(self.envs.step_flags, non_blocking=True)
+        if self.envs.device.type == "cuda":
+            self.t.cuda.current_stream(self.envs.device).synchronize()
+        n = self.envs.n
+        f = self.flags.numpy()
+        return o.numpy(), f[:4 * n].view(np.float32), f[4 * n:5 * n], f[5 * n:6 * n]
+
+    def done_rows(self, idx: np.ndarray):
+        """terminal obs, episode return / length of the lanes in idx (small device gathers)."""
+        e, t = self.envs, self.t
+        i = t.as_tensor(idx, dtype=t.int64).to(e.device, non_blocking=True)
+        return (e.terminal_obs.index_select(0, i).cpu().numpy(), e.ep_return.index_select(0, i).cpu().numpy(),
+                e.ep_len.index_select(0, i).cpu().numpy())
+
+
+class F16VecEnv(*_bases(SB3VecEnv)):
     """Vectorised drop-in for ``DummyVecEnv([lambda: Monitor(gym.make("JSBSim-v0"))] * N)``.
 
     Honours the SB3 VecEnv contract (base_vec_env.py:50-357): ``reset() -> obs``,
     ``step_async/step_wait -> (obs, rews, dones, infos)``, auto-reset with
     ``infos[i]["terminal_observation"]`` and ``infos[i]["TimeLimit.truncated"]``
     (dummy_vec_env.py:56-73), Monitor's ``infos[i]["episode"] = {r, l, t}``
-    (monitor.py:96-109), ``seed()`` applied at the next reset (:292-309).
-    ``return_numpy=False`` keeps everything on the GPU (infos list is then omitted: the
-    caller reads ``last_step`` device tensors)."""
+    (monitor.py:96-109), ``seed()`` applied at the next reset (:292-309). When
+    stable_baselines3 is importable this class IS a ``VecEnv`` subclass, so
+    ``BaseAlgorithm._wrap_env`` (base_class.py:215) takes it as-is.
+
+    Numpy mode (default, what SB3 consumes): one pinned-memory copy of obs and one of the
+    packed rewards/flags per step, one stream sync; infos of lanes that did not finish share one
+    read-only dict. The obs array returned stays valid for two further steps (see _HostStaging).
+    ``return_numpy=False`` keeps everything on the GPU (infos is then None: the caller reads the
+    ``last_step`` device tensors). ``envs=`` wraps an existing handle instead of creating one."""
 
     metadata = {"render_modes": []}
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
-                 return_numpy: bool = True, env_id_base: int = 0, **kw):
-        self.num_envs = int(num_envs)
-        self.envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, env_id_base=env_id_base, **kw)
-        self.observation_space = spaces.observation_space(stack_k)
-        self.action_space = spaces.action_space()
+                 return_numpy: bool = True, env_id_base: int = 0, envs=None, **kw):
+        self.envs = envs if envs is not None else F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed,
+                                                          env_id_base=env_id_base, **kw)
+        n = self.envs.n
         self.render_mode = None
+        self._attrs: dict = {}
+        obs_space, act_space = spaces.observation_space(self.envs.k), spaces.action_space()
+        if SB3VecEnv is not None:
+            SB3VecEnv.__init__(self, n, obs_space, act_space)  # base_vec_env.py:59-94
+        else:
+            self.num_envs = n
+            self.observation_space, self.action_space = obs_space, act_space
+            self.reset_infos: list = [{} for _ in range(n)]
+            self._seeds: list = [None for _ in range(n)]
+            self._options: list = [{} for _ in range(n)]
         self.return_numpy = bool(return_numpy)
-        self.reset_infos: list = [{} for _ in range(self.num_envs)]
-        self._seeds: list = [None for _ in range(self.num_envs)]
-        self._options: list = [{} for _ in range(self.num_envs)]
+        self._host = _HostStaging(self.envs) if self.return_numpy else None
         self._actions = None
         self._t_start = time.time()
         self.last_step: Optional[StepOut] = None
-        self._attrs: dict = {}
 
     # -- VecEnv API -------------------------------------------------------------------------
     def reset(self):
         goals = None
         if any(s is not None for s in self._seeds):
-            # seeded lanes follow the reference's numpy stream; unseeded lanes use the device RNG
-            dev_goals = None
-            if not all(s is not None for s in self._seeds):
-                self.envs.reset()  # draw device goals for every lane first
-                dev_goals = self.envs.get_state()[:, 62:65].float().cpu().numpy()
-            goals = np.zeros((self.num_envs, 3), np.float32)
+            # seeded lanes follow the reference's numpy stream (jsbsim_gym.py:312-323); NaN rows
+            # draw the device goal, all in ONE reset (each lane's episode counter advances once)
+            goals = np.full((self.num_envs, 3), np.nan, np.float32)
             for i, s in enumerate(self._seeds):
-                goals[i] = reference_goal(s) if s is not None else dev_goals[i]
+                if s is not None:
+                    goals[i] = reference_goal(s)
         obs = self.envs.reset(goals=goals)
         self._seeds = [None for _ in range(self.num_envs)]
         self._options = [{} for _ in range(self.num_envs)]
         self.reset_infos = [{} for _ in range(self.num_envs)]
-        return obs.cpu().numpy() if self.return_numpy else obs
+        self._t_start = time.time()
+        if not self.return_numpy:
+            return obs
+        return self._host.fetch(obs, with_flags=False)[0]
 
     def step_async(self, actions) -> None:
         self._actions = actions
 
     def step_wait(self):
-        out = self.envs.step(self._actions)
-        self.last_step = out
         if not self.return_numpy:
-            dones = (out.terminated | out.truncated).bool()
-            return out.obs, out.rew, dones, None
-        obs = out.obs.cpu().numpy()
-        rew = out.rew.cpu().numpy()
-        term_u8 = out.terminated.cpu().numpy()
-        term = term_u8.astype(bool)
-        trunc = out.truncated.cpu().numpy().astype(bool)
-        dones = term | trunc
-        infos = [{"TimeLimit.truncated": False} for _ in range(self.num_envs)]
+            out = self.envs.step(self._actions)
+            self.last_step = out
+            return out.obs, out.rew, (out.terminated | out.truncated).bool(), None
+        out = self.envs.step(self._host.actions_to_device(self._actions))
+        self.last_step = out
+        obs, rew, term_u8, trunc_u8 = self._host.fetch(out.obs)
+        dones = (term_u8 | trunc_u8).astype(bool)
+        infos = [_NOT_DONE_INFO] * self.num_envs
         idx = np.flatnonzero(dones)
         if idx.size:
-            tobs = out.terminal_obs[idx].cpu().numpy()
-            eret = out.ep_return[idx].cpu().numpy()
-            elen = out.ep_len[idx].cpu().numpy()
+            tobs, eret, elen = self._host.done_rows(idx)
             t = round(time.time() - self._t_start, 6)
-            for j, i in enumerate(idx):
-                infos[i]["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
-                infos[i]["terminal_observation"] = tobs[j]
-                infos[i]["episode"] = {"r": round(float(eret[j]), 6), "l": int(elen[j]), "t": t}
+            for j, i in enumerate(idx.tolist()):
+                info = {"TimeLimit.truncated": bool(trunc_u8[i] and not term_u8[i]),
+                        "terminal_observation": tobs[j],
+                        "episode": {"r": round(float(eret[j]), 6), "l": int(elen[j]), "t": t}}
                 if term_u8[i] & 2:  # NaN guard quarantine (nan_guard=True)
-                    infos[i]["nonfinite"] = True
-        return obs, rew, dones, infos
+                    info["nonfinite"] = True
+                infos[i] = info
+        return obs, rew.copy(), dones, infos
 
     def step(self, actions):
         self.step_async(actions)
@@ -409,22 +517,52 @@ class F16VecEnv:
             return [indices]
         return indices
 
+    # per-lane attributes of the reference env (jsbsim_gym.py:103-118), read from the device state
+    _LANE_ATTRS = ("current_step", "goal", "state")
+    _CONST_ATTRS = {"num_stacked_frames": "k", "max_episode_steps": None, "down_sample": None, "dg": None}
+
     def get_attr(self, attr_name: str, indices=None) -> list:
+        idx = list(self._indices(indices))
         if attr_name in self._attrs:
-            v = self._attrs[attr_name]
-        elif attr_name in ("render_mode", "observation_space", "action_space", "metadata"):
-            v = getattr(self, attr_name)
-        elif attr_name == "spec":
-            v = None
-        else:
-            raise AttributeError(attr_name)
-        return [v for _ in self._indices(indices)]
+            return [self._attrs[attr_name] for _ in idx]
+        if attr_name in ("render_mode", "observation_space", "action_space", "metadata"):
+            return [getattr(self, attr_name) for _ in idx]
+        if attr_name == "spec":
+            return [None for _ in idx]
+        c = self.envs.cfg
+        const = {"num_stacked_frames": self.envs.k, "max_episode_steps": int(c.max_steps),
+                 "down_sample": int(c.down_sample), "dg": float(c.dg_m)}
+        if attr_name in const:
+            return [const[attr_name] for _ in idx]
+        if attr_name in self._LANE_ATTRS:
+            from .abi import F16C_GOAL, F16C_STEP
+            if attr_name == "state":  # jsbsim_gym.py:181-193: newest frame's 12 state values
+                rows = self.envs.obs[:, -1, :12].index_select(0, self.envs.torch.as_tensor(idx, device=self.envs.device))
+                return list(rows.cpu().numpy())
+            st = self.envs.get_state().cpu().numpy()
+            if attr_name == "current_step":
+                return [int(st[i, F16C_STEP]) for i in idx]
+            return [st[i, F16C_GOAL:F16C_GOAL + 3].astype(np.float32) for i in idx]
+        raise AttributeError(attr_name)
 
     def set_attr(self, attr_name: str, value: Any, indices=None) -> None:
         self._attrs[attr_name] = value
 
     def env_method(self, method_name: str, *method_args, indices=None, **method_kwargs) -> list:
-        raise AttributeError("F16VecEnv lanes expose no per-env methods (%s)" % method_name)
+        """The single-env methods that make sense on device lanes: render (no renderer: None,
+        like an env without render_mode), get_wrapper_attr (gymnasium >= 1.0 attribute access),
+        reset (the indexed lanes, new goals from the device stream)."""
+        idx = list(self._indices(indices))
+        if method_name == "render":
+            return [None for _ in idx]
+        if method_name == "get_wrapper_attr":
+            return self.get_attr(method_args[0], idx)
+        if method_name == "reset":
+            mask = np.zeros(self.num_envs, np.uint8)
+            mask[idx] = 1
+            obs = self.envs.reset(mask=mask)[self.envs.torch.as_tensor(idx, device=self.envs.device)]
+            return [(o, {}) for o in obs.cpu().numpy()]
+        raise AttributeError("F16VecEnv lanes have no per-env method %r" % method_name)
 
     def env_is_wrapped(self, wrapper_class, indices=None) -> list:
         name = getattr(wrapper_class, "__name__", str(wrapper_class))
@@ -434,7 +572,7 @@ class F16VecEnv:
 
     def has_attr(self, attr_name: str) -> bool:
         try:
-            self.get_attr(attr_name)
+            self.get_attr(attr_name, 0)
             return True
         except AttributeError:
             return False
@@ -450,11 +588,12 @@ class F16VecEnv:
         return self
 
 
-class F16GymVectorEnv:
+class F16GymVectorEnv(*_bases(GymVectorEnv)):
     """gymnasium.vector.VectorEnv surface over the same kernel (the north star's "Gymnasium
-    VectorEnv step()/reset()"), for gymnasium-native learners; duck-typed (gymnasium is not a
-    dependency). Autoreset mode SAME_STEP -- what the kernel does: a lane that terminates or
-    truncates returns its reset observation in the same step, and
+    VectorEnv step()/reset()"), for gymnasium-native learners; a VectorEnv subclass when
+    gymnasium is importable (registered as "JSBSim-v0"'s vector entry point,
+    f16_jsb_amd/__init__.py). Autoreset mode SAME_STEP -- what the kernel does: a lane that
+    terminates or truncates returns its reset observation in the same step, and
 
       infos["final_obs"] / infos["_final_obs"]   final (K,15) observation / mask
       infos["episode"] = {"r", "l", "t"}, infos["_episode"]   (RecordEpisodeStatistics keys)
@@ -467,10 +606,10 @@ class F16GymVectorEnv:
     metadata = {"autoreset_mode": "SameStep", "render_modes": []}
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
-                 return_numpy: bool = True, **kw):
-        self.num_envs = int(num_envs)
-        self.envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
-        self.single_observation_space = spaces.observation_space(stack_k)
+                 return_numpy: bool = True, envs=None, **kw):
+        self.envs = envs if envs is not None else F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
+        self.num_envs = self.envs.n
+        self.single_observation_space = spaces.observation_space(self.envs.k)
         self.single_action_space = spaces.action_space()
         self.observation_space = spaces.batch_space(self.single_observation_space, self.num_envs)
         self.action_space = spaces.batch_space(self.single_action_space, self.num_envs)
@@ -478,10 +617,8 @@ class F16GymVectorEnv:
         self.spec = None
         self.closed = False
         self.return_numpy = bool(return_numpy)
+        self._host = _HostStaging(self.envs) if self.return_numpy else None
         self._t_start = time.time()
-
-    def _out(self, t):
-        return t.cpu().numpy() if self.return_numpy else t
 
     def reset(self, *, seed=None, options=None):
         goals = None
@@ -489,30 +626,50 @@ class F16GymVectorEnv:
             seeds = [seed + i for i in range(self.num_envs)] if isinstance(seed, int) else list(seed)
             if len(seeds) != self.num_envs:
                 raise ValueError("need one seed per env")
-            if any(s is None for s in seeds):
-                self.envs.reset()
-                dev_goals = self.envs.get_state()[:, 62:65].float().cpu().numpy()
-            goals = np.stack([reference_goal(s) if s is not None else dev_goals[i] for i, s in enumerate(seeds)])
+            goals = np.full((self.num_envs, 3), np.nan, np.float32)  # NaN rows: device goal
+            for i, s in enumerate(seeds):
+                if s is not None:
+                    goals[i] = reference_goal(s)
         obs = self.envs.reset(goals=goals)
         self._t_start = time.time()
-        return self._out(obs), {}
+        if not self.return_numpy:
+            return obs, {}
+        return self._host.fetch(obs, with_flags=False)[0], {}
 
     def step(self, actions):
-        out = self.envs.step(actions)
-        term, trunc = out.terminated.bool(), out.truncated.bool()
+        if not self.return_numpy:
+            out = self.envs.step(actions)
+            term, trunc = out.terminated.bool(), out.truncated.bool()
+            done = term | trunc
+            infos = {}
+            if bool(done.any()):
+                t = round(time.time() - self._t_start, 6)
+                infos["final_obs"] = out.terminal_obs.clone()
+                infos["_final_obs"] = done
+                infos["episode"] = {"r": t_where(done, out.ep_return, 0.0), "l": t_where(done, out.ep_len, 0),
+                                    "t": t_where(done, t, 0.0)}
+                infos["_episode"] = done
+            return out.obs, out.rew, term, trunc, infos
+        out = self.envs.step(self._host.actions_to_device(actions))
+        obs, rew, term_u8, trunc_u8 = self._host.fetch(out.obs)
+        term, trunc = term_u8.astype(bool), trunc_u8.astype(bool)
         done = term | trunc
         infos = {}
-        if bool(done.any()):
+        idx = np.flatnonzero(done)
+        if idx.size:
             t = round(time.time() - self._t_start, 6)
-            mask = done.cpu().numpy()
-            infos["final_obs"] = self._out(out.terminal_obs.clone())
-            infos["_final_obs"] = mask
-            eret = out.ep_return.cpu().numpy()
-            elen = out.ep_len.cpu().numpy()
-            infos["episode"] = {"r": np.where(mask, np.round(eret, 6), 0.0), "l": np.where(mask, elen, 0),
-                                "t": np.where(mask, t, 0.0)}
-            infos["_episode"] = mask
-        return self._out(out.obs), self._out(out.rew), self._out(term), self._out(trunc), infos
+            tobs, eret, elen = self._host.done_rows(idx)
+            final = np.zeros_like(obs)
+            final[idx] = tobs
+            r = np.zeros(self.num_envs)
+            r[idx] = np.round(eret, 6)
+            ln = np.zeros(self.num_envs, np.int32)
+            ln[idx] = elen
+            infos["final_obs"] = final
+            infos["_final_obs"] = done
+            infos["episode"] = {"r": r, "l": ln, "t": np.where(done, t, 0.0)}
+            infos["_episode"] = done
+        return obs, rew.copy(), term, trunc, infos
 
     def close(self, **kwargs):
         if not self.closed:
@@ -525,3 +682,66 @@ class F16GymVectorEnv:
     @property
     def unwrapped(self):
         return self
+
+
+def t_where(mask, x, other):
+    import torch
+    if not isinstance(x, torch.Tensor):
+        x = torch.full(mask.shape, float(x), device=mask.device)
+    return torch.where(mask, x, torch.as_tensor(other, dtype=x.dtype, device=x.device))
+
+
+class F16GymEnv(*_bases(GymEnv)):
+    """ONE env with the single-env gymnasium surface of ``gym.make("JSBSim-v0")``
+    (jsbsim_gym.py:537-545: JSBSimEnv wrapped in PositionReward(1e-2), TimeLimit(1200)) over a
+    one-lane handle: ``reset(seed, options) -> (obs (K,15), {})`` with the default_rng(seed)
+    goal of jsbsim_gym.py:312-323 (seed None: the device goal stream), ``step(action) ->
+    (obs, reward, terminated, truncated, {})``, no auto-reset (the caller resets, as with the
+    reference). A gymnasium.Env subclass when gymnasium is importable; the entry point
+    "JSBSim-v0" is registered to (f16_jsb_amd/__init__.py), so an unchanged train.py gets a
+    GPU-backed env from gym.make -- one env, SB3 then wraps it in Monitor + DummyVecEnv as it
+    does the reference's. For throughput use F16VecEnv."""
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, stack_k: int = 10, device=None, seed: int = 0, envs=None, **kw):
+        self.envs = envs if envs is not None else F16Envs(1, stack_k=stack_k, device=device, seed=seed,
+                                                          autoreset=False, **kw)
+        self.observation_space = spaces.observation_space(self.envs.k)
+        self.action_space = spaces.action_space()
+        self.render_mode = None
+        self._host = _HostStaging(self.envs, ring=2)
+
+    def reset(self, *, seed=None, options=None):
+        if GymEnv is not None:
+            GymEnv.reset(self, seed=seed)  # gymnasium's np_random seeding (jsbsim_gym.py:302)
+        goals = None if seed is None else reference_goal(seed)[None]
+        obs = self.envs.reset(goals=goals)
+        return self._host.fetch(obs, with_flags=False)[0][0].copy(), {}
+
+    def step(self, action):
+        out = self.envs.step(self._host.actions_to_device(np.asarray(action, np.float32).reshape(1, 4)))
+        obs, rew, term, trunc = self._host.fetch(out.obs)
+        return obs[0].copy(), float(rew[0]), bool(term[0]), bool(trunc[0]), {}
+
+    def render(self):
+        return None
+
+    def close(self):
+        self.envs.close()
+
+    @property
+    def unwrapped(self):
+        return self
+
+
+def make_gym_env(**kw) -> F16GymEnv:
+    """gymnasium entry point of "JSBSim-v0" (jsbsim_gym.py:537-545 wrap_jsbsim counterpart)."""
+    kw.pop("root", None)  # JSBSimEnv(root=...) names a JSBSim data directory: nothing to load here
+    return F16GymEnv(**kw)
+
+
+def make_gym_vector_env(num_envs: int = 1, **kw) -> F16GymVectorEnv:
+    """gymnasium vector entry point of "JSBSim-v0" (gymnasium.make_vec)."""
+    kw.pop("root", None)
+    return F16GymVectorEnv(num_envs=num_envs, **kw)

@@ -200,9 +200,15 @@ def rebuild_observations(frames, obs0, episode_starts, k: int, steps=None):
 def gather_to_rank0(buf: DeviceRolloutBuffer, group=None, chunk_steps: Optional[int] = None,
                     fields=FIELDS) -> Optional[Dict[str, torch.Tensor]]:
     """Gather every rank's rollout shard to rank 0 (RCCL over xGMI on MI355X, gloo in CPU
-    tests). Returns on rank 0 a dict of (n_steps, world*n_envs, ...) tensors (env axis
-    rank-major, matching env_id_base = rank * n_envs) plus 'obs0'; None on other ranks.
-    Gathers are chunked over steps (chunk_steps) to bound the staging memory."""
+    tests). Returns on rank 0 a dict of RANK-MAJOR tensors (world, n_steps, n_envs, ...) -- rank
+    r's shard at [r], i.e. global envs [r * n_envs, (r + 1) * n_envs) as env_id_base assigns them
+    -- plus 'obs0' (world, n_envs, K, 15); None on other ranks. ``env_major`` turns a field into
+    the (n_steps, world * n_envs, ...) layout of a single-GPU buffer.
+
+    The output is allocated once and every collective writes straight into it: chunk [t0, t1)
+    of rank r lands in the contiguous view out[r, t0:t1], so rank 0 moves each byte once (no
+    per-chunk temporaries, no strided re-copy). Gathers are chunked over steps (chunk_steps) to
+    bound each collective's size; a short last chunk is fine."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
@@ -212,21 +218,21 @@ def gather_to_rank0(buf: DeviceRolloutBuffer, group=None, chunk_steps: Optional[
     out = {}
     for f in tuple(fields) + ("obs0",):
         x = getattr(buf, f)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        res = torch.empty((world,) + tuple(x.shape), dtype=x.dtype, device=x.device) if rank == 0 else None
         if f == "obs0":
-            parts = [torch.empty_like(x) for _ in range(world)] if rank == 0 else None
-            dist.gather(x.contiguous(), parts, dst=0, group=group)
-            if rank == 0:
-                out[f] = torch.cat(parts, dim=0)
-            continue
-        res = torch.empty((T, world * buf.n_envs) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device) if rank == 0 else None
-        for t0 in range(0, T, chunk):
-            t1 = min(T, t0 + chunk)
-            piece = x[t0:t1].contiguous()
-            parts = [torch.empty_like(piece) for _ in range(world)] if rank == 0 else None
-            dist.gather(piece, parts, dst=0, group=group)
-            if rank == 0:
-                for r in range(world):
-                    res[t0:t1, r * buf.n_envs:(r + 1) * buf.n_envs] = parts[r]
+            dist.gather(x, list(res.unbind(0)) if rank == 0 else None, dst=0, group=group)
+        else:
+            for t0 in range(0, T, chunk):
+                t1 = min(T, t0 + chunk)
+                dist.gather(x[t0:t1], [res[r, t0:t1] for r in range(world)] if rank == 0 else None, dst=0, group=group)
         if rank == 0:
             out[f] = res
     return out if rank == 0 else None
+
+
+def env_major(x: torch.Tensor) -> torch.Tensor:
+    """(world, T, N, ...) rank-major gather output -> (T, world * N, ...) (a copy)."""
+    w, T, N = x.shape[:3]
+    return x.transpose(0, 1).reshape((T, w * N) + tuple(x.shape[3:]))

@@ -173,7 +173,8 @@ size_t f16env_state_bytes(f16env_t h);
 int f16env_state_bytes_per_env(void);
 
 /* Reset the lanes where mask[i] != 0 (mask NULL = all).
- *   goals: N x 3 float (x, y, alt in m) or NULL -> device Philox goal RNG
+ *   goals: N x 3 float (x, y, alt in m) or NULL -> device Philox goal RNG; a row whose x is
+ *          NaN also takes the device goal (seeded and unseeded lanes in one call)
  *   ic:    N x F16_IC_N double or NULL -> the config's default IC (template copy)
  *   obs:   N x K x 15 float; rows of reset lanes are written (K copies of frame 0). */
 int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goals,

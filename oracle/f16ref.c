@@ -73,6 +73,21 @@ typedef struct {
 static consts_t K;
 static int K_ready = 0;
 
+/* Test-only physics switch (f16ref_set_physics_mask, default 0 = the full model): drops the
+ * aerodynamic forces and moments, the thrust, gravity, or J2 (central gravity only), so CPU
+ * tests can check the equations of motion against analytic invariants
+ * (tests/test_oracle_physics.py). Process-wide; tests set it around their own runs. */
+static int g_phys_mask = 0;
+void f16ref_set_physics_mask(int mask) { g_phys_mask = mask; }
+static void init_consts(void);
+/* body inertia (slug ft^2, incl. pilot and the pinned tanks) and mass (slug), for tests */
+void f16ref_mass_props(double J[9], double* mass) {
+  init_consts();
+  memcpy(J, K.J, sizeof K.J);
+  *mass = K.mass;
+}
+int f16ref_get_physics_mask(void) { return g_phys_mask; }
+
 /* ------------------------------------------------------------------------------------------
  * small linear algebra (row-major 3x3)
  * ---------------------------------------------------------------------------------------- */
@@ -453,7 +468,7 @@ static void derive(const env_t* e, derived_t* d) {
 static void gravity_j2(const derived_t* d, double* g) {
   double r = d->r, sl = d->slat;
   double adivr = WGS_A / r;
-  double pre = 1.5 * J2_E * adivr * adivr;
+  double pre = (g_phys_mask & F16REF_PHYS_NO_J2) ? 0.0 : 1.5 * J2_E * adivr * adivr;
   double xy = 1.0 - 5.0 * sl * sl, z = 3.0 - 5.0 * sl * sl;
   double gm = GM_E / (r * r);
   g[0] = -gm * (1.0 + pre * xy) * d->rE[0] / r;
@@ -514,6 +529,19 @@ static double aero_scale(double in, double inmin, double inmax, double outmin, d
   if (in == 0.0) return 0.0;
   if (in > 0.0) return (in / inmax) * outmax;
   return (in / inmin) * outmin;
+}
+
+/* the FCS / engine components as stand-alone entry points for unit tests */
+double f16ref_kinematic(double out, double in, const double* detents, const double* times, int n, double dt,
+                        int ic) {
+  return kinematic(out, in, detents, times, n, dt, ic);
+}
+double f16ref_pid(double in, double* integral, double* prev, double trigger, double kp, double ki, double kd,
+                  double dt, int ic) {
+  return pid(in, integral, prev, trigger, kp, ki, kd, dt, ic);
+}
+double f16ref_aero_scale(double in, double inmin, double inmax, double outmin, double outmax) {
+  return aero_scale(in, inmin, inmax, outmin, outmax);
 }
 
 typedef struct { double de, da, dr, dlef, flap_mix, dsb, throttle; } fcs_out_t;
@@ -603,6 +631,9 @@ static double seek(double v, double target, double accel, double decel, double d
   else if (v < target) { v += dt * accel; if (v > target) v = target; }
   return v;
 }
+double f16ref_seek(double v, double target, double accel, double decel, double dt) {
+  return seek(v, target, accel, decel, dt);
+}
 static double engine_run(env_t* e, double throttle_pos, double mach, double h_rho, double sigma,
                          double dt, int ic) {
   const double milthrust = 17800.0, maxthrust = 29000.0, bleed = 0.03;
@@ -685,6 +716,7 @@ static void frame(env_t* e, double dt, int ic, frame_diag_t* diag) {
   /* Inertial */
   double gE[3];
   gravity_j2(&d, gE);
+  if (g_phys_mask & F16REF_PHYS_NO_GRAVITY) gE[0] = gE[1] = gE[2] = 0.0;
   /* Atmosphere (standard day: density altitude == geometric altitude) */
   double atm[4];
   f16ref_atmosphere(d.h_ft, atm);
@@ -725,6 +757,7 @@ static void frame(env_t* e, double dt, int ic, frame_diag_t* diag) {
   e->lx[F16L_NPY] = npy; e->lx[F16L_NPZ] = npz;
   /* Propulsion */
   double thrust = engine_run(e, fc.throttle, mach, d.h_ft, sigma, dt, ic);
+  if (g_phys_mask & F16REF_PHYS_NO_THRUST) thrust = 0.0;
   /* Aerodynamics: data-driven products over the XML function list (f16.xml:986-1917) */
   double P[RP_COUNT];
   P[RP_aero_qbar_psf] = qbar; P[RP_metrics_Sw_sqft] = S_W; P[RP_metrics_bw_ft] = B_W;
@@ -746,6 +779,8 @@ static void frame(env_t* e, double dt, int ic, frame_diag_t* diag) {
     else v *= tab2(f->table, P[f->tvar[0]], f->tvar[1] >= 0 ? P[f->tvar[1]] : 0.0);
     ax[f->axis] += v;
   }
+  if (g_phys_mask & F16REF_PHYS_NO_AERO)
+    for (int k = 0; k < 6; k++) ax[k] = 0.0;
   /* wind axes (D, Y, L) -> body: vFw = (-D, Y, -L), vForces = Tw2b * vFw */
   double ca = cos(alpha), sa = sin(alpha), cb = cos(beta), sb = sin(beta);
   double Fw[3] = {-ax[AX_DRAG], ax[AX_SIDE], -ax[AX_LIFT]};
@@ -999,7 +1034,9 @@ int f16ref_reset(f16ref* h, const uint8_t* mask, const float* goals, const doubl
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < h->n; i++) {
     if (mask && !mask[i]) continue;
-    env_reset(h, i, goals ? goals + 3 * i : NULL, ic ? ic + (size_t)F16_IC_N * i : NULL);
+    const float* g = goals ? goals + 3 * i : NULL;
+    if (g && isnan(g[0])) g = NULL; /* NaN row: device-stream goal (include/f16env.h) */
+    env_reset(h, i, g, ic ? ic + (size_t)F16_IC_N * i : NULL);
     if (obs) write_stack(h, &h->env[i], obs + (size_t)KO * i);
   }
   return 0;

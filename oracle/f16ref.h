@@ -50,6 +50,25 @@ double f16ref_vcas_kts(double mach, double p_psf);
  * (for table known-answer tests): returns the table value at (x, y). */
 double f16ref_aero_table(int fn_index, double x, double y);
 int f16ref_n_aero_fns(void);
+/* TEST-ONLY physics switch (default 0 = full model; process-wide): bits drop the
+ * aerodynamic forces/moments, the thrust, gravity, or gravity's J2 term, for analytic
+ * invariant tests of the equations of motion. */
+#define F16REF_PHYS_NO_AERO 0x1
+#define F16REF_PHYS_NO_THRUST 0x2
+#define F16REF_PHYS_NO_GRAVITY 0x4
+#define F16REF_PHYS_NO_J2 0x8
+void f16ref_set_physics_mask(int mask);
+int f16ref_get_physics_mask(void);
+void f16ref_mass_props(double J[9], double* mass);
+/* FCS / engine components for unit tests: FGKinematic traverse (detents/times, n entries),
+ * FGPID (integral / previous input updated in place), aerosurface_scale (zero-centred),
+ * FGTurbine's rate-limited Seek. */
+double f16ref_kinematic(double out, double in, const double* detents, const double* times, int n, double dt,
+                        int ic);
+double f16ref_pid(double in, double* integral, double* prev, double trigger, double kp, double ki, double kd,
+                  double dt, int ic);
+double f16ref_aero_scale(double in, double inmin, double inmax, double outmin, double outmax);
+double f16ref_seek(double v, double target, double accel, double decel, double dt);
 /* Number of OpenMP threads the batch loops use (1 if built without OpenMP). */
 int f16ref_threads(void);
 

@@ -52,6 +52,15 @@ def lib():
         L.f16ref_aero_table.restype = dp
         L.f16ref_n_aero_fns.restype = i32
         L.f16ref_threads.restype = i32
+        L.f16ref_set_physics_mask.argtypes = [i32]
+        L.f16ref_get_physics_mask.restype = i32
+        L.f16ref_mass_props.argtypes = [vp, vp]
+        for name in ("f16ref_kinematic", "f16ref_pid", "f16ref_aero_scale", "f16ref_seek"):
+            getattr(L, name).restype = dp
+        L.f16ref_kinematic.argtypes = [dp, dp, vp, vp, i32, dp, i32]
+        L.f16ref_pid.argtypes = [dp, vp, vp, dp, dp, dp, dp, dp, i32]
+        L.f16ref_aero_scale.argtypes = [dp, dp, dp, dp, dp]
+        L.f16ref_seek.argtypes = [dp, dp, dp, dp, dp]
         _lib = L
     return _lib
 

@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from f16_jsb_amd.rollout import DeviceRolloutBuffer, bootstrap_timeouts, gather_to_rank0, rebuild_observations
+from f16_jsb_amd.rollout import DeviceRolloutBuffer, bootstrap_timeouts, env_major, gather_to_rank0, rebuild_observations
 
 
 def _simulate_stacks(T, N, K, rng):
@@ -73,7 +73,7 @@ def test_bootstrap_timeouts_semantics():
     np.testing.assert_array_equal(out.numpy(), want)
 
 
-def _gather_worker(rank, world, path, T, N, K, q):
+def _gather_worker(rank, world, path, T, N, K, chunk, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     dist.init_process_group("gloo", init_method="file://" + path, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(100 + rank)
@@ -84,7 +84,7 @@ def _gather_worker(rank, world, path, T, N, K, q):
                 (torch.rand(N, generator=g) < 0.2).float(), torch.randn(N, generator=g), torch.randn(N, generator=g))
     buf.advantages.copy_(torch.randn(T, N, generator=g))
     buf.returns.copy_(buf.advantages + buf.values)
-    out = gather_to_rank0(buf, chunk_steps=3)
+    out = gather_to_rank0(buf, chunk_steps=chunk)
     local = {k: v.clone() for k, v in buf.state_dict().items()}
     if rank == 0:
         q.put(("out", {k: v.numpy() for k, v in out.items()}))
@@ -95,13 +95,16 @@ def _gather_worker(rank, world, path, T, N, K, q):
     dist.destroy_process_group()
 
 
-def test_gather_to_rank0_gloo_world2():
-    T, N, K, world = 7, 6, 4, 2
+@pytest.mark.parametrize("world,chunk", [(2, 3), (3, 3)], ids=["world2", "world3_uneven_chunk"])
+def test_gather_to_rank0_gloo(world, chunk):
+    """Rank-major gather into one preallocated output: out[f][r] == rank r's shard, bit for bit,
+    with T = 7 steps in chunks of 3 (3 + 3 + 1: a short last chunk)."""
+    T, N, K = 7, 6, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "rdzv")
-        procs = [ctx.Process(target=_gather_worker, args=(r, world, path, T, N, K, q)) for r in range(world)]
+        procs = [ctx.Process(target=_gather_worker, args=(r, world, path, T, N, K, chunk, q)) for r in range(world)]
         for p in procs:
             p.start()
         got = dict(q.get(timeout=120) for _ in range(world + 1))
@@ -110,9 +113,9 @@ def test_gather_to_rank0_gloo_world2():
             assert p.exitcode == 0
     out = got["out"]
     for f, v in out.items():
-        if f == "obs0":
-            want = np.concatenate([got["local%d" % r][f] for r in range(world)], axis=0)
-        else:
-            want = np.concatenate([got["local%d" % r][f] for r in range(world)], axis=1)
+        want = np.stack([got["local%d" % r][f] for r in range(world)])
         np.testing.assert_array_equal(v, want, err_msg=f)
-    assert out["frames"].shape == (T, world * N, 15)
+        if f != "obs0":  # the single-GPU (T, world * N) layout
+            np.testing.assert_array_equal(env_major(torch.as_tensor(v)).numpy(),
+                                          np.concatenate([got["local%d" % r][f] for r in range(world)], axis=1))
+    assert out["frames"].shape == (world, T, N, 15) and out["obs0"].shape == (world, N, K, 15)

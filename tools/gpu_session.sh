@@ -30,7 +30,8 @@ run() {  # run <name> <timeout> <cmd...>
 python -c "from f16_jsb_amd.build import build; build()" || exit 3
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -x ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    prodtests) run pytest_prod 600 python -u -m pytest tests/test_gpu_production.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 50 ;;
     stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
