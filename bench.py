@@ -372,8 +372,8 @@ def sb3_compat_bench(dev, n, steps=20):
     venv = F16VecEnv(num_envs=n, stack_k=10, device=dev, seed=5, return_numpy=True)
     venv.reset()
     rng = np.random.default_rng(0)
-    acts = [torch.as_tensor(rng.uniform([-1, -1, -1, 0], [1, 1, 1, 1], (n, 4)).astype(np.float32), device=dev)
-            for _ in range(4)]
+    # numpy actions, as SB3's collect_rollouts hands them over (on_policy_algorithm.py:210-218)
+    acts = [rng.uniform([-1, -1, -1, 0], [1, 1, 1, 1], (n, 4)).astype(np.float32) for _ in range(4)]
     for t in range(3):
         venv.step(acts[t % 4])
     torch.cuda.synchronize()
@@ -384,7 +384,8 @@ def sb3_compat_bench(dev, n, steps=20):
     venv.close()
     return {"envs": n, "stack_k": 10, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
             "env_steps_per_s": round(n * steps / el, 1),
-            "note": "numpy obs/rew/dones + N info dicts per step (SB3 VecEnv contract), device actions"}
+            "note": "numpy actions in; numpy obs/rew/dones + N infos out per step (SB3 VecEnv contract, "
+                    "PCIe-inclusive: pinned staging, one obs + one packed flag copy, shared info for running lanes)"}
 
 
 def load_traffic(envs, stack, state_bytes):
