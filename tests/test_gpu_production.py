@@ -73,7 +73,9 @@ def _assert_frames_stat(gpu, ref, tol, tol_max, what):
     assert bad.size == 0, "%s: 99.9th percentile of component %d = %.3e > %.1e" % (what, bad[0], p[bad[0]], tol[bad[0]])
 
 
-def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None):
+def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None, early=None):
+    """early = (step, tol): every lane's newest frame within tol at that step (before the
+    chaotic growth of the fp32-vs-fp64 difference sets in)."""
     tol_max = tol_final if tol_max is None else tol_max
     n = ref.n
     done_idx = torch.zeros(n, dtype=torch.int32, device=g.device)
@@ -102,6 +104,8 @@ def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None)
             assert np.all(og == og[:, :1]), "reset rows are K copies of frame 0"
             np.testing.assert_array_equal(og[:, :, 12:], o_r[d][:, :, 12:])  # Philox goals
             _assert_frames(og[:, -1], o_r[d][:, -1], TOL_STEP, "reset frame @%d" % t)
+        if early is not None and t == early[0]:
+            _assert_frames(out.obs.cpu().numpy()[:, -1], o_r[:, -1], early[1], "all lanes @%d" % t)
     o_g = out.obs.cpu().numpy()
     _report("final frames", o_g[:, -1], o_r[:, -1])
     _assert_frames_stat(o_g[:, -1], o_r[:, -1], tol_final, tol_max, "frames @%d" % steps)
@@ -145,12 +149,16 @@ def test_cfg5_production_instance_131072(torch_mod):
     np.testing.assert_array_equal(o_g[:, :, 12:], o[:, :, 12:])
     _assert_frames(o_g[:, -1], o[:, -1], TOL_STEP, "random-IC reset")
     _stagger(ref, g, o)
-    # 99.9 % of the lanes within TOL_RAND30 * 2 (tests/test_gpu_cfg5.py's gust tolerance: the
-    # per-step gust draws differ by up to 1e-4 fps, fp32 Box-Muller vs fp64), every lane within
-    # 4 x TOL_RAND30: the random-IC box reaches 30 000 ft / 1 200 fps and +-10 deg attitudes,
-    # where random actions amplify fp32 round-off fastest; over 131 072 lanes the worst lane at
-    # 30 steps reached beta 6.7e-5 rad, p 2.7e-4 rad/s, phi 1.2e-4 rad (MI355X run r02b)
-    fin = _run_parity(torch, ref, g, 30, 23, TOL_RAND30 * 2, gust=True, tol_max=TOL_RAND30 * 4)
+    # Every lane within TOL_RAND30 at step 10; at step 30, 99.9 % of the lanes within
+    # TOL_RAND30 * 2 (the per-step gust draws differ by up to 1e-4 fps, fp32 Box-Muller vs
+    # fp64, tests/test_gpu_cfg5.py) and every lane within 10 x TOL_RAND30. The random-IC box
+    # reaches 1 200 fps: the worst lanes are transonic (mach 1.02-1.11) at 1-3 km, where the
+    # difference starts at fp32 round-off (~1e-7 at step 1) and grows ~10x per 10 steps
+    # (chaos). profiles/r02_cfg5_tail.json (tools/cfg5_tail.py, MI355X): worst of
+    # 131 072 lanes at step 30 p 3.0e-3 rad/s, r 3.2e-3, phi 2.7e-4 rad, beta 1.9e-4; at step
+    # 10 p 3.6e-6. The one-wave build (F16ENV_OCC=1) and a second handle are bit-identical.
+    fin = _run_parity(torch, ref, g, 30, 23, TOL_RAND30 * 2, gust=True, tol_max=TOL_RAND30 * 10,
+                      early=(10, TOL_RAND30))
     assert fin >= n // 3
     ref.close()
     g.close()
