@@ -65,6 +65,7 @@ struct ModelConsts {
   float rho_sl, a_sl, p_sl;  // US-76 sea level (slug/ft3, ft/s, psf)
   float inv_rho_sl, inv_p_sl;
   float kts_per_fps;
+  float qc_vc250, qc_vc20, qc_vc10, qc_vc5;  // impact pressure (psf) at these calibrated airspeeds (kts)
   double cos_dE, sin_dE;     // rotation of the Earth per frame (omega * dt)
   double dt;
 };
@@ -370,21 +371,27 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
   return o;
 }
 
-// FGAuxiliary::VcalibratedFromMach (kts)
-__device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts& C) {
-#ifdef F16_DIAG_NO_VCAS  // timing ablation only
-  return 600.0f * mach;
-#endif
+// FGAuxiliary::VcalibratedFromMach, split in two. The FCS reads velocities/vc-kts only
+// through four thresholds (f16.xml: TEF switch 250 kts, PID triggers 20 / 5 / 10 kts), and
+// the calibrated airspeed is a monotone function of the impact pressure qc = pt - p, so the
+// frame latches qc (psf) and the FCS compares it with the qc of each threshold
+// (ModelConsts::qc_vc*, computed in fp64 at create); vc itself (kts) is evaluated from the
+// latch only where it is reported (f16env_get_state).
+__device__ __forceinline__ float impact_pressure(float mach, float p) {
   if (!(fabsf(mach) > 0.0f)) return 0.0f;
   float pt;
   if (mach < 1.0f) {
     float x = 1.0f + 0.2f * mach * mach;
     pt = p * (x * x * x * fsqrt(x));
-  } else {
+  } else {  // Rayleigh pitot
     float m2 = mach * mach, d = 7.0f * m2 - 1.0f;
     pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * fsqrt(d));
   }
-  const float qc = pt - p;
+  return pt - p;
+}
+// calibrated airspeed (kts) from the latched impact pressure
+__device__ __forceinline__ float vcas_from_qc(float qc, const ModelConsts& C) {
+  if (!(qc != 0.0f)) return 0.0f;
   const float A = qc * C.inv_p_sl + 1.0f;
   float M = fsqrt(5.0f * (__builtin_amdgcn_exp2f((1.0f / 3.5f) * __builtin_amdgcn_logf(A)) - 1.0f));
   if (M > 1.0f) {
@@ -406,6 +413,20 @@ __device__ __forceinline__ float vcas_kts(float mach, float p, const ModelConsts
     M = fsqrt(y);
   }
   return C.a_sl * M * C.kts_per_fps;
+}
+
+// inverse of vcas_from_qc (fp64): the impact pressure of a calibrated airspeed, for
+// f16env_set_state's canonical vc-kts latch
+__device__ __forceinline__ float qc_from_vcas(double vc_kts, const ModelConsts& C) {
+  const double m = vc_kts / (double)C.kts_per_fps / (double)C.a_sl;
+  double A;
+  if (m < 1.0) {
+    A = pow(1.0 + 0.2 * m * m, 3.5);
+  } else {
+    const double d = 7.0 * m * m - 1.0;
+    A = 166.92158009316827 * pow(m, 7.0) / pow(d, 2.5);
+  }
+  return (float)((A - 1.0) * (double)C.p_sl);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -577,9 +598,11 @@ __device__ __forceinline__ void euler(const float* T, float& phi, float& tht, fl
   } else if (T[2] >= 1.0f) {
     tht = -0.5f * PI_F; phi = atan2f(-T[7], T[4]); psi = 0.0f;
   } else {
-    tht = asinf(-T[2]);
-    phi = atan2f(T[5], T[8]);
-    float p = atan2f(T[1], T[0]);
+    // theta = asin(-T13) as atan2(-T13, cos theta) with cos theta = |(T23, T33)| (Tl2b is a
+    // rotation); the polynomial atan2 (|err| < 1e-7 rad) instead of OCML's asinf / atan2f
+    tht = fatan2(-T[2], fsqrt(T[5] * T[5] + T[8] * T[8]));
+    phi = fatan2(T[5], T[8]);
+    float p = fatan2(T[1], T[0]);
     if (p < 0.0f) p += 2.0f * PI_F;
     psi = p;
   }
@@ -590,41 +613,36 @@ __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fmi
 __device__ __forceinline__ bool eq_roundoff(float a, float b) {
   return fabsf(a - b) <= 2.0f * 1.1920929e-07f * fmaxf(fabsf(a), fabsf(b));
 }
-// FGKinematic with two detents (single segment): rate = (d1 - d0) / t. Branch-free.
+// FGKinematic with two detents (single segment): rate = (d1 - d0) / t. The traverse moves
+// the output toward the (clamped) input by at most dt * rate per frame, which is the oracle's
+// "dt < |in - out| / rate ? out +- dt rate : in" as one clamp of the difference (the reached
+// value is out + (in - out), within an ulp of in). Branch-free.
 __device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float rate, float dt,
                                       bool ic) {
   in = clipf(in, d0, d1);
   if (ic) return in;  // compile-time after inlining
-  const float tdt = fabsf((in - out) * (1.0f / rate));
-  const float step = (out < in) ? dt * rate : -dt * rate;
-  const float moved = (dt < tdt) ? out + step : in;
+  const float lim = dt * rate;
+  const float moved = out + clipf(in - out, -lim, lim);
   return eq_roundoff(in, out) ? out : moved;
 }
-// TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350). The FGKinematic
-// while-loop needs at most three passes here (segment [-1,0] is instantaneous); unrolled,
-// branch-free.
+// TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350), the FGKinematic
+// while-loop of oracle kinematic() in closed form. Segment [-1, 0] has transition time 0 (the
+// output jumps to the input whenever the traverse starts in it), segment [0, 1] moves at 1/3
+// per second, so at most two passes run: a partial or complete move inside [0, 1], then, if
+// time is left and the input is negative, the jump from 0 to it.
 __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic) {
   in = clipf(in, -1.0f, 1.0f);
   if (ic) return in;
-  float dt0 = dt;
-  bool active = true;
-#pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    active = active && dt0 > 0.0f && !eq_roundoff(in, out);
-    if (__ballot(active) == 0) break;  // wave-uniform: the flaps are at their detent
-    const bool down = in < out;
-    const bool seg1 = down ? !(0.0f < out) : !(0.0f <= out);  // transition time 0 -> jump
-    const float tin = clipf(in, 0.0f, 1.0f);
-    const float tdt = fabsf((tin - out) * 3.0f);               // / rate, rate = 1/3
-    const bool partial = dt0 < tdt;
-    const float step = (out < in) ? dt0 * (1.0f / 3.0f) : -dt0 * (1.0f / 3.0f);
-    const float o1 = seg1 ? in : (partial ? out + step : tin);
-    const float d1 = (seg1 || partial) ? 0.0f : dt0 - tdt;
-    out = active ? o1 : out;
-    dt0 = active ? d1 : dt0;
-    active = active && !seg1;
-  }
-  return out;
+  const bool down = in < out;
+  const bool seg1 = down ? !(0.0f < out) : !(0.0f <= out);  // first pass in [-1, 0]: jump
+  const float tin = clipf(in, 0.0f, 1.0f);
+  const float tdt = fabsf((tin - out) * 3.0f);               // / rate, rate = 1/3
+  const bool partial = dt < tdt;
+  const float step = (out < in) ? dt * (1.0f / 3.0f) : -dt * (1.0f / 3.0f);
+  // second pass: output at 0 (tin), time left, input below it -> jump to the input
+  const bool jump2 = (dt - tdt > 0.0f) && !eq_roundoff(in, tin);
+  const float o = seg1 ? in : (partial ? out + step : (jump2 ? in : tin));
+  return eq_roundoff(in, out) ? out : o;
 }
 __device__ __forceinline__ float pidf(float in, float& itot, float& prev, float trig, float kp,
                                       float ki, float kd, float dt, bool ic) {
@@ -660,7 +678,8 @@ __device__ __forceinline__ FcsTab fcs_tables(const Lane& L, const float* T) {
 
 // f16.xml:309-984 (document order). T = LDS table blob.
 __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33, float v_fps,
-                                        const float* T, const FcsTab& tb, float dt, bool ic, FcsOut& o) {
+                                        const float* T, const FcsTab& tb, const ModelConsts& C, float dt, bool ic,
+                                        FcsOut& o) {
 #ifdef F16_DIAG_NO_FCS  // timing ablation only: surfaces follow the commands directly
   if (!ic) {
     o.de = cmd[1] * 0.436f; o.da = cmd[0] * 0.375f; o.dr = cmd[2] * 0.524f; o.dlef = 0.0f; o.flap_mix = 0.0f;
@@ -668,15 +687,15 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
     return;
   }
 #endif
-  const float alpha = L.lx[F16L_ALPHA], mach = L.lx[F16L_MACH], vc = L.lx[F16L_VC_KTS];
+  // qc: the impact-pressure latch (vcas_from_qc); "vc < V kts" is "qc < qc(V)"
+  const float alpha = L.lx[F16L_ALPHA], mach = L.lx[F16L_MACH], qc = L.lx[F16L_VC_KTS];
   // Flaps
-  float tef_rad = 0.0f;
-  if (vc < 250.0f) tef_rad = 0.349f;
-  else if (mach > 0.9f) tef_rad = -0.0349f;
-  L.tef = kin_tef(L.tef, tef_rad * 2.864789f, dt, ic);
+  // switch (:319-327) as selects of the normalised command (tef_rad * 2.864789)
+  const float tef_norm = (qc < C.qc_vc250) ? 0.349f * 2.864789f : ((mach > 0.9f) ? -0.0349f * 2.864789f : 0.0f);
+  L.tef = kin_tef(L.tef, tef_norm, dt, ic);
   // Roll
   const float roll_err = cmd[0] - L.lx[F16L_P_AERO] * 0.31821f;
-  const float ail_trig = (vc < 20.0f) ? 0.0f : 1.0f;
+  const float ail_trig = (qc < C.qc_vc20) ? 0.0f : 1.0f;
   const float roll_pid = pidf(roll_err, L.pri, L.prp, ail_trig, 3.0f, 0.0005f, -0.00125f, dt, ic);
   const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
   o.da = aero_scale(roll_cmd, 0.375f);
@@ -690,23 +709,20 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
   const float ele_sched = ele_lim * tb.ele;
   const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
-  const float ele_trig = (vc < 5.0f) ? 0.0f : 1.0f;
+  const float ele_trig = (qc < C.qc_vc5) ? 0.0f : 1.0f;
   const float gpid = clipf(pidf(pitch_err, L.ppi, L.ppp, ele_trig, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
   const float pitch_sched = clipf(ele_sched + alpha * 1.0472f + gpid, -1.0f, 1.0f);
   L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
   o.de = aero_scale(L.ele, 0.436f);
   // Yaw
   const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tb.yaw + L.lx[F16L_NPY] * 0.25f;
-  const float rud_trig = (vc < 10.0f) ? 0.0f : 1.0f;
+  const float rud_trig = (qc < C.qc_vc10) ? 0.0f : 1.0f;
   const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, rud_trig, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
   const float yaw_sched = clipf(cmd[2] + ypid, -1.0f, 1.0f);
   L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, 2.0f / 0.4f, dt, ic);
   o.dr = aero_scale(L.rud, 0.524f);
   // Leading edge flap (gear pinned up, no WOW)
-  float lef_rad = 0.0f;
-  if (alpha > 0.2618f) lef_rad = 0.436f;
-  else if (alpha > 0.0873f) lef_rad = 0.262f;
-  else if (mach > 0.9f) lef_rad = -0.0349f;
+  const float lef_rad = (alpha > 0.2618f) ? 0.436f : ((alpha > 0.0873f) ? 0.262f : ((mach > 0.9f) ? -0.0349f : 0.0f));
   o.dlef = lef_rad;
   L.lef = kin2(L.lef, lef_rad * 2.293578f, -1.0f, 1.0f, 2.0f / 3.0f, dt, ic);
   // Throttle
@@ -981,7 +997,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F16_STAMP(stamps, ST_ATM);
   // -- Systems (reads the previous frame's latch) --
   FcsOut fc;
-  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, tb, dt, ic, fc);
+  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, tb, C, dt, ic, fc);
   F16_STAMP(stamps, ST_FCS);
   // -- Propulsion --
   const float thrust = engine_run(L, fc.throttle, mach, h, sigma, T, dt, ic);
@@ -1027,7 +1043,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   // -- Auxiliary latch for the next frame's FCS --
   if (LOWREG) __builtin_amdgcn_sched_barrier(0);
   L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;
-  L.lx[F16L_VC_KTS] = vcas_kts(mach, atm.P, C); L.lx[F16L_VG_FPS] = vg;
+  L.lx[F16L_VC_KTS] = impact_pressure(mach, atm.P); L.lx[F16L_VG_FPS] = vg;
   L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
   L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
   F16_STAMP(stamps, ST_ACCEL);

@@ -984,7 +984,7 @@ __global__ void f16_ic_kernel(SoA dst, const double* ic, ModelConsts C) {
     dst.c[NCOL_ALL + j] = make_float4(f[4 * j], f[4 * j + 1], f[4 * j + 2], f[4 * j + 3]);
 }
 
-__global__ void f16_get_state_kernel(SoA s, double* c) {
+__global__ void f16_get_state_kernel(SoA s, double* c, ModelConsts C) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= s.n) return;
   Lane L;
@@ -1007,11 +1007,12 @@ __global__ void f16_get_state_kernel(SoA s, double* c) {
   o[F16C_PID_P_P] = L.ppp; o[F16C_PID_Y_I] = L.pyi; o[F16C_PID_Y_P] = L.pyp;
   o[F16C_N1] = L.n1; o[F16C_N2] = L.n2; o[F16C_AUG] = (L.flags & LANE_FLAG_AUG) ? 1.0 : 0.0;
   for (int j = 0; j < F16L_N; ++j) o[F16C_LX + j] = L.lx[j];
+  o[F16C_LX + F16L_VC_KTS] = vcas_from_qc(L.lx[F16L_VC_KTS], C);  // the latch holds qc
   o[F16C_LAST_D] = L.last_d; o[F16C_STEP] = L.step; o[F16C_EP_RET] = L.ep_ret;
   o[F16C_EP_COUNT] = (double)(uint32_t)L.ep_count;
 }
 
-__global__ void f16_set_state_kernel(SoA s, const double* c) {
+__global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= s.n) return;
   Lane L;
@@ -1035,6 +1036,7 @@ __global__ void f16_set_state_kernel(SoA s, const double* c) {
   L.n1 = (float)o[F16C_N1]; L.n2 = (float)o[F16C_N2];
   L.flags = o[F16C_AUG] != 0.0 ? LANE_FLAG_AUG : 0;
   for (int j = 0; j < F16L_N; ++j) L.lx[j] = (float)o[F16C_LX + j];
+  L.lx[F16L_VC_KTS] = qc_from_vcas(o[F16C_LX + F16L_VC_KTS], C);
   L.last_d = (float)o[F16C_LAST_D]; L.step = (int32_t)o[F16C_STEP]; L.ep_ret = o[F16C_EP_RET];
   L.ep_count = (int32_t)(uint32_t)o[F16C_EP_COUNT];
   lane_store<true>(s, k, L);
@@ -1321,6 +1323,14 @@ static void build_consts(const f16env_config& cfg, ModelConsts& C) {
   C.inv_rho_sl = (float)(1.0 / (101325.0 / (R * 288.15) / 515.3788183931961));
   C.inv_p_sl = (float)(47.88025898033584 / 101325.0);
   C.kts_per_fps = (float)(1.0 / (1852.0 / (3600.0 * 0.3048)));
+  // impact pressure at the FCS's calibrated-airspeed thresholds (f16.xml: TEF switch, PID
+  // triggers), subsonic pitot (all four are far below calibrated Mach 1)
+  const double a_sl = sqrt(1.4 * R * 288.15) / 0.3048, p_sl = 101325.0 / 47.88025898033584;
+  auto qc_at = [&](double kts) {
+    const double m = kts * (1852.0 / (3600.0 * 0.3048)) / a_sl;
+    return (float)(p_sl * (pow(1.0 + 0.2 * m * m, 3.5) - 1.0));
+  };
+  C.qc_vc250 = qc_at(250.0); C.qc_vc20 = qc_at(20.0); C.qc_vc10 = qc_at(10.0); C.qc_vc5 = qc_at(5.0);
   C.dt = cfg.dt;
   C.cos_dE = cos(OMEGA_E * cfg.dt);
   C.sin_dE = sin(OMEGA_E * cfg.dt);
@@ -1643,14 +1653,14 @@ int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step
 
 int f16env_get_state(f16env_t h, void* stream, double* canon) {
   if (!h || !canon) return set_err(-1, "null argument");
-  hipLaunchKernelGGL(f16_get_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon);
+  hipLaunchKernelGGL(f16_get_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon, h->C);
   HIPCHK(hipGetLastError());
   return 0;
 }
 
 int f16env_set_state(f16env_t h, void* stream, const double* canon) {
   if (!h || !canon) return set_err(-1, "null argument");
-  hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon);
+  hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon, h->C);
   HIPCHK(hipGetLastError());
   return 0;
 }
