@@ -99,6 +99,9 @@ static constexpr float RAD2DEG_F = 57.295779513082320876798f;
 //   C6  aI.z aIp.xyz           C13 pid_y_p n1 n2 lx0      C19 gust.xyz, 0 (cfg5 gust mode only)
 enum { NCOL = 19, NCOL_ALL = 20, COL_GUST = 19 };
 static constexpr int LANE_FLAG_AUG = 1;
+// set by every reset path, cleared by the next step: the windowed-observation step fills the
+// lane's new history window with its reset frame (f16env_step_window)
+static constexpr int LANE_FLAG_FRESH = 2;
 // persistent bytes per env moved by a step (SURVEY.md 8d "S"); +16 in gust mode
 static constexpr int STATE_BYTES = NCOL * 16;
 static constexpr int STATE_BYTES_GUST = NCOL_ALL * 16;

@@ -348,6 +348,7 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
+  L.flags |= LANE_FLAG_FRESH;
   make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
   L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
 }
@@ -365,6 +366,7 @@ __device__ __forceinline__ void lane_reset_template(Lane& L, const float4* sTmpl
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
+  L.flags |= LANE_FLAG_FRESH;
 #ifdef F16_RESET_MAKE_FRAME  // A/B only: evaluate frame 0 per finished lane
   make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
 #else
@@ -455,6 +457,12 @@ struct StepArgs {
   float* r_act;                // N x 4: the actions applied
   float* r_rew;                // N: rewards
   float* r_next_start;         // N: done as 0/1 float (episode_starts of the next slot)
+  // windowed observations (f16env_step_window): the frame histories of this step (wx, the one
+  // whose window is the returned observation) and of the other parity (wy), [N][T][15] each
+  float* wx;
+  float* wy;
+  int64_t wrow;                // floats per env row = T * 15
+  int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
   EnvArgs E;
   ModelConsts C;
 };
@@ -474,7 +482,41 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
 // frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
 // 160 KB). sT is then unused.
-template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false>
+// Windowed observations (WIN, f16env_step_window): per env two frame histories [T][15] (wx:
+// this step's parity, wy: the other), the observation of a step being the view
+// wx[k][p-K+1 .. p] (strides T*15, 15, 1). A step writes its new frame at position p of BOTH
+// histories -- no stack shift copy, no previous-stack read -- with 16-B stores at the
+// position's uniform phase (put_frame). Lanes reset right before this step (FRESH) fill
+// wx[p-K+1 .. p-1] with their reset frame (LDS-DMA'd from wy[p-1], which that reset wrote);
+// lanes reset by this step fill wx[p-K+1 .. p] with the new reset frame and keep their final
+// frame in wy[p], so wy's window IS the terminal observation (no copy). The other parity's
+// window is untouched by a step, so an observation stays valid until the step after next, as
+// with the ping-pong buffers of f16env_step.
+// One frame (15 floats) to a history row at float phase pf = (frame start mod 4), uniform per
+// launch: whole 16-B stores between a 1-3 float head and tail (4 or 5 store instructions).
+typedef float f2s __attribute__((ext_vector_type(2)));
+typedef float f3s __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void put_frame(float* d, const float* f, int pf) {
+  auto q4 = [&](int o, int j) { *reinterpret_cast<float4*>(d + o) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]); };
+  if (pf == 0) {
+    q4(0, 0); q4(4, 4); q4(8, 8);
+    *reinterpret_cast<f3s*>(d + 12) = f3s{f[12], f[13], f[14]};
+  } else if (pf == 1) {
+    *reinterpret_cast<f3s*>(d) = f3s{f[0], f[1], f[2]};
+    q4(3, 3); q4(7, 7); q4(11, 11);
+  } else if (pf == 2) {
+    *reinterpret_cast<f2s*>(d) = f2s{f[0], f[1]};
+    q4(2, 2); q4(6, 6); q4(10, 10);
+    d[14] = f[14];
+  } else {
+    d[0] = f[0];
+    q4(1, 1); q4(5, 5); q4(9, 9);
+    *reinterpret_cast<f2s*>(d + 13) = f2s{f[13], f[14]};
+  }
+}
+static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([15][64])
+
+template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
@@ -528,6 +570,21 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   issue_stack_dma();
 #endif
   if (ROLL && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
+  // a lane reset since the last step: the windowed step reads its reset frame (wy[p-1]) now,
+  // so the load streams in behind the physics
+  // (LDS-DMA into the wave's staging area, [15][64] floats, not registers: nothing stays live
+  // across the frames; the vmcnt(0) after the frames retires it)
+  bool fresh = false;
+  float* stg = dynl + (size_t)wave * WFRESH;
+  if (live) {
+    fresh = (L.flags & LANE_FLAG_FRESH) != 0;
+    L.flags &= ~LANE_FLAG_FRESH;
+  }
+  if (WIN && fresh && a.E.K > 1) {
+    const float* src = a.wy + k * a.wrow + (int64_t)(a.wpos - 1) * F16_OBS_DIM;
+#pragma unroll
+    for (int j = 0; j < F16_OBS_DIM; ++j) dma4(src + j, stg + j * 64);
+  }
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   float rew_out = 0.0f;
@@ -638,7 +695,30 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       for (int c = 0; c < F16_OBS_DIM; ++c) a.r_frame[k * F16_OBS_DIM + c] = a.obs_prev[k * KC + HC + c];
     }
   }
-  if (kSkipStack) {
+  if (WIN) {
+    const int K = a.E.K, p = a.wpos;
+    const bool reset_now = live && done && autoreset;
+    if (live && K > 1 && (fresh || reset_now)) {  // rare: whole-window fills of reset lanes
+      float* X = a.wx + k * a.wrow;
+      if (fresh) {
+        float f0p[F16_OBS_DIM];
+#pragma unroll
+        for (int j = 0; j < F16_OBS_DIM; ++j) f0p[j] = stg[j * 64 + lane];
+        for (int r = p - K + 1; r < p; ++r) put_frame(X + (int64_t)r * F16_OBS_DIM, f0p, (4 - (r & 3)) & 3);
+      }
+      if (reset_now)  // after the fresh fill: a one-step episode ends in its own reset window
+        for (int r = p - K + 1; r < p; ++r) put_frame(X + (int64_t)r * F16_OBS_DIM, f0, (4 - (r & 3)) & 3);
+    }
+    // this step's frame at position p of both histories (wx: the reset frame of a lane reset
+    // now, else the new frame; wy: the new frame), aligned stores at the uniform phase
+    if (live) {
+      const int pf = (4 - (p & 3)) & 3;
+      const int64_t off = k * a.wrow + (int64_t)p * F16_OBS_DIM;
+      put_frame(a.wx + off, reset_now ? f0 : f, pf);
+      put_frame(a.wy + off, f, pf);
+    }
+    F16_STAMP(stamps, ST_COPY);
+  } else if (kSkipStack) {
   } else if (image) {
     // 2) splice the new frame of row r into the image at row r+1's first frame, which the
     //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block. The stack
@@ -784,7 +864,21 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
   extern __shared__ __align__(16) float dynl[];
   step_body<MODE, true, ROLL>(a, nullptr, sTmpl, sDone, dynl);
 }
+// windowed-observation build (f16env_step_window): no stack image, LDS holds the tables and
+// the per-wave frame staging
+template <int MODE, int OCC>
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_kernel(StepArgs a) {
+  STEP_SHARED
+  step_body<MODE, false, false, OCC == 2, true>(a, sT, sTmpl, sDone, dynl);
+}
 using StepKernel = void (*)(StepArgs);
+static StepKernel step_win_kernel_for(int mode, int occ) {
+  static const StepKernel table[2][4] = {
+      {f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
+      {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}};
+  return table[occ == 2 ? 1 : 0][mode & 3];
+}
+static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WFRESH;
 // variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
 // roll: the rollout-slot build (f16env_step_rollout); the plain step carries none of its code.
 static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {
@@ -861,7 +955,7 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
   for (int t = 0; t < a.T; ++t) {
     const float4 av = philox_action(a.seed, gid, a.step0 + (uint64_t)t);
     const float cmd[4] = {av.x, av.y, av.z, av.w};
-    L.step += 1;                                              // jsbsim_gym.py:215
+    L.step += 1;  L.flags &= ~LANE_FLAG_FRESH;                                              // jsbsim_gym.py:215
     double ce, se;
     earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);
@@ -912,7 +1006,8 @@ struct ResetDoneArgs {
   SoA s, tmpl;
   const int32_t* done_idx;
   const int32_t* n_done;
-  float* obs;
+  float* obs;       // row of env k: obs + k * obs_row + obs_off (contiguous: K*15, 0; window: T*15, (p-K+1)*15)
+  int64_t obs_row, obs_off;
   EnvArgs E;
   ModelConsts C;
 };
@@ -929,7 +1024,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
     float f0[F16_OBS_DIM];
     lane_reset(L, a.tmpl, nullptr, nullptr, a.E, k, sT, a.C, f0);
     lane_store<true>(a.s, k, L);
-    float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;
+    float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
       for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
   }
@@ -940,7 +1035,8 @@ struct ResetArgs {
   const uint8_t* mask;
   const float* goals;
   const double* ic;
-  float* obs;
+  float* obs;       // row addressing as ResetDoneArgs
+  int64_t obs_row, obs_off;
   EnvArgs E;
   ModelConsts C;
 };
@@ -960,10 +1056,22 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, g, a.E, k, sT, a.C, f0);
   lane_store<true>(a.s, k, L);
   if (a.obs) {
-    float* o = a.obs + k * (int64_t)a.E.K * F16_OBS_DIM;
+    float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
       for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
   }
+}
+
+// windowed observations: the histories' last K-1 frames (positions p_old-K+2 .. p_old) move
+// to the front (0 .. K-2) of both histories, so the next step writes its frame at K-1
+__global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wrow, int32_t p_old, float* h0, float* h1) {
+  const int64_t per = (int64_t)(K - 1) * F16_OBS_DIM;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * n * per) return;
+  const int64_t b = i / (n * per), r = i - b * n * per;
+  const int64_t k = r / per, j = r - k * per;
+  float* row = (b ? h1 : h0) + k * wrow;
+  row[j] = row[(int64_t)(p_old - K + 2) * F16_OBS_DIM + j];
 }
 
 // IC -> state (used once at create to build the reset template, n = 1)
@@ -1255,6 +1363,7 @@ struct f16env {
   unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine counter (device, 8 B)
   int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 GUSTS
   int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
+  int win_occ;        // the same for the windowed-observation step kernel
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
@@ -1450,6 +1559,8 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     const int64_t waves = ((int64_t)cfg->n_envs + 63) / 64;
     h->occ = (!h->gt && waves > 4 * (int64_t)cus && 2 * (static_lds + h->dyn_lds) <= 160 * 1024) ? 2 : 1;
     if (getenv("F16ENV_OCC")) h->occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
+    h->win_occ = (waves > 4 * (int64_t)cus && 2 * (static_lds + WIN_DYN_LDS) <= 160 * 1024) ? 2 : 1;
+    if (getenv("F16ENV_OCC")) h->win_occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
     for (int v = 0; v <= 2; ++v) {
       const size_t st_v = v == 2 ? static_gt : static_lds;
       for (int m = 0; m < 8; ++m) {
@@ -1537,6 +1648,7 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   if (!h) return set_err(-1, "null handle");
   ResetArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = obs;
+  a.obs_row = (int64_t)h->cfg.stack_k * F16_OBS_DIM; a.obs_off = 0;
   a.E = env_args(h);
   a.C = h->C;
   hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
@@ -1566,6 +1678,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   float* feat = slot ? slot->features : nullptr;
   if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
     return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
+  a.wx = a.wy = nullptr; a.wrow = 0; a.wpos = 0;
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = h->lds_image;
@@ -1589,6 +1702,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = obs;
+    r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1609,6 +1723,93 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
   return step_impl(h, stream, nullptr, act, obs_prev, obs, rew, terminated, truncated, terminal_obs, ep_return,
                    ep_len, done_idx, n_done);
 }
+
+static int window_check(f16env_t h, const float* hist_cur, const float* hist_other, int64_t T, int32_t pos) {
+  const int K = h->cfg.stack_k;
+  if (!hist_cur || (hist_other == nullptr && hist_cur == nullptr)) return set_err(-1, "null history");
+  if (((uintptr_t)hist_cur & 15) != 0 || ((uintptr_t)hist_other & 15) != 0)
+    return set_err(-1, "histories must be 16-byte aligned");
+  if (T % 4 != 0 || T < 2 * (int64_t)K) return set_err(-1, "history length T must be a multiple of 4 and >= 2K");
+  if (pos < K - 1 || (int64_t)pos >= T) return set_err(-1, "window position must be in [K-1, T-1]");
+  return 0;
+}
+
+int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_cur, float* hist_other, int64_t T,
+                       int32_t pos, float* rew, uint8_t* terminated, uint8_t* truncated, double* ep_return,
+                       int32_t* ep_len, int32_t* done_idx, int32_t* n_done) {
+  if (!h) return set_err(-1, "null handle");
+  if (!act || !hist_other || !rew || !terminated || !truncated)
+    return set_err(-1, "act/hist_cur/hist_other/rew/terminated/truncated are required");
+  if (int e = window_check(h, hist_cur, hist_other, T, pos)) return e;
+  if (hist_cur == hist_other) return set_err(-1, "the two histories must be distinct buffers");
+  if (done_idx && !n_done) return set_err(-1, "done_idx requires n_done");
+  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  StepArgs a;
+  memset(&a, 0, sizeof a);
+  a.s = h->soa; a.tmpl = h->tmpl; a.act = act; a.rew = rew;
+  a.term = terminated; a.trunc = truncated; a.ep_ret = ep_return; a.ep_len = ep_len;
+  a.done_idx = done_idx; a.n_done = n_done;
+  a.nonfinite = h->nonfinite;
+  a.wx = hist_cur; a.wy = hist_other; a.wrow = T * F16_OBS_DIM; a.wpos = pos;
+  a.E = env_args(h);
+  a.C = h->C;
+  a.lds_image = 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (h->mode && !done_idx) {
+    a.done_idx = h->done_buf;
+    a.n_done = h->done_buf + h->cfg.n_envs;
+  }
+  if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
+  const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
+  const StepKernel kern = step_win_kernel_for(h->mode, h->win_occ);
+  if (h->prof_next < (int)h->prof_ev.size() / 2) {
+    const int i = h->prof_next++;
+    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)WIN_DYN_LDS, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u, a);
+  } else {
+    hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, a);
+  }
+  HIPCHK(hipGetLastError());
+  if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
+    ResetDoneArgs r;
+    r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
+    r.obs_row = T * F16_OBS_DIM; r.obs_off = (int64_t)(pos - a.E.K + 1) * F16_OBS_DIM;
+    r.E = a.E; r.C = h->C;
+    const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
+    hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
+int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
+                        float* hist_cur, int64_t T, int32_t pos) {
+  if (!h) return set_err(-1, "null handle");
+  if (int e = window_check(h, hist_cur, nullptr, T, pos)) return e;
+  ResetArgs a;
+  a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = hist_cur;
+  a.obs_row = T * F16_OBS_DIM; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * F16_OBS_DIM;
+  a.E = env_args(h);
+  a.C = h->C;
+  hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, int64_t T, int32_t pos_old) {
+  if (!h) return set_err(-1, "null handle");
+  if (!hist1) return set_err(-1, "null history");
+  if (int e = window_check(h, hist0, hist1, T, pos_old)) return e;
+  const int K = h->cfg.stack_k;
+  if (K < 2) return 0;
+  if (pos_old - K + 2 <= K - 2) return set_err(-1, "restart source and destination overlap (pos_old < 2K-3)");
+  const int64_t total = 2 * (int64_t)h->cfg.n_envs * (K - 1) * F16_OBS_DIM;
+  hipLaunchKernelGGL(f16_window_restart_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (int64_t)h->cfg.n_envs, (int32_t)K, T * F16_OBS_DIM, pos_old, hist0, hist1);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_step_window_waves_per_simd(f16env_t h) { return h ? h->win_occ : 0; }
 
 int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                         const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,

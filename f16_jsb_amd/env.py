@@ -50,7 +50,14 @@ class F16Envs:
 
     def __init__(self, n_envs: int, stack_k: int = 10, device=None, seed: int = 0,
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
-                 autoreset: bool = True, ic=None, nan_guard: bool = False, **cfg_kw):
+                 autoreset: bool = True, ic=None, nan_guard: bool = False, obs_layout: str = "contiguous",
+                 history: int = 0, **cfg_kw):
+        """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
+        obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
+        `history` frames (f16env_step_window: only the new frame is written per step; strides
+        (T*15, 15, 1), so obs.reshape(N, K*15) is still a view); history 0 = max(128, 4K)
+        rounded up to a multiple of 4. Both layouts give identical values and the same
+        validity (an observation stays valid until the step after next)."""
         import torch
 
         if not torch.cuda.is_available():
@@ -73,7 +80,21 @@ class F16Envs:
         self._h = h
         f32, dev = torch.float32, self.device
         n, k = self.n, self.k
-        self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
+        if obs_layout not in ("contiguous", "window"):
+            raise ValueError("obs_layout must be 'contiguous' or 'window'")
+        self.window = obs_layout == "window"
+        if self.window:
+            T = int(history) if history else max(128, 4 * k)
+            T = (T + 3) // 4 * 4
+            if T < 2 * k:
+                raise ValueError("history must be >= 2 * stack_k")
+            self.T = T
+            self._hist = torch.zeros((2, n, T, F16_OBS_DIM), dtype=f32, device=dev)
+            self._hist_ptr = (self._hist[0].data_ptr(), self._hist[1].data_ptr())
+            self._p = k - 1   # newest frame position of the current observation's window
+            self._obs = None
+        else:
+            self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
         self._cur = 0
         # rewards (f32), terminated, truncated (u8) in ONE allocation, so a host-side consumer
         # (F16VecEnv's numpy mode) moves the three with a single device-to-host copy
@@ -82,14 +103,21 @@ class F16Envs:
         self.rew = self.step_flags[:4 * n].view(f32)
         self.term = self.step_flags[4 * n:5 * n]
         self.trunc = self.step_flags[5 * n:6 * n]
-        self.terminal_obs = torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev)
+        # window layout: terminal_obs is re-pointed at the other history's window every step
+        self.terminal_obs = None if self.window else torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev)
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
         self._act = torch.zeros((n, 4), dtype=f32, device=dev)
         # the handle's own buffers never move: their addresses are taken once, not per step
-        self._obs_ptr = [o.data_ptr() for o in self._obs]
-        self._out_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
-                         self.terminal_obs.data_ptr(), self.ep_return.data_ptr(), self.ep_len.data_ptr())
+        if self.window:
+            self._win_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
+                             self.ep_return.data_ptr(), self.ep_len.data_ptr())
+            self._step_win_fn = L.f16env_step_window
+            self.terminal_obs = self._window(1)
+        else:
+            self._obs_ptr = [o.data_ptr() for o in self._obs]
+            self._out_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
+                             self.terminal_obs.data_ptr(), self.ep_return.data_ptr(), self.ep_len.data_ptr())
         self._step_fn = L.f16env_step
 
     # --------------------------------------------------------------------------------------
@@ -99,9 +127,18 @@ class F16Envs:
     def _stream_int(self) -> int:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
+    def _window(self, other: int = 0):
+        """(N, K, 15) view of the current (other=0) or other-parity history's window."""
+        p = self._p
+        return self._hist[self._cur ^ other, :, p - self.k + 1:p + 1]
+
+    def _no_window(self, what: str):
+        if self.window:
+            raise F16EnvError("%s is not available with obs_layout='window' (use obs_layout='contiguous')" % what)
+
     @property
     def obs(self):
-        return self._obs[self._cur]
+        return self._window() if self.window else self._obs[self._cur]
 
     def close(self):
         if getattr(self, "_h", None):
@@ -117,11 +154,15 @@ class F16Envs:
     @property
     def waves_per_simd(self) -> int:
         """Occupancy the step kernel variant of this handle is built for (1 or 2)."""
+        if self.window:
+            return int(lib().f16env_step_window_waves_per_simd(self._h))
         return int(lib().f16env_step_waves_per_simd(self._h))
 
     @property
     def step_kernel_name(self) -> str:
         mode = (1 if self.cfg.flags & F16_FLAG_RANDOM_IC else 0) | (2 if self.cfg.flags & F16_FLAG_GUSTS else 0)
+        if self.window:
+            return "f16_step_win_kernel<%d, %d>" % (mode, self.waves_per_simd)
         variant = int(lib().f16env_step_variant(self._h))
         if variant == 2:
             return "f16_step_gt_kernel<%d>" % mode
@@ -149,6 +190,10 @@ class F16Envs:
             raise ValueError("goals must be (N, 3)")
         if c is not None and tuple(c.shape) != (self.n, F16_IC_N):
             raise ValueError("ic must be (N, %d)" % F16_IC_N)
+        if self.window:
+            check(lib().f16env_reset_window(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c),
+                                            self._hist_ptr[self._cur], self.T, self._p), "f16env_reset_window")
+            return self._window()
         out = self._obs[self._cur]
         check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
         return out
@@ -171,6 +216,8 @@ class F16Envs:
         the policy features of the returned obs (features.py:37-67) in the same call."""
         if features is not None:
             return self.step_rollout(0, 0, features=features, policy_actions=actions)
+        if self.window:
+            return self._step_window(actions, done_idx, n_done)
         t = self.torch
         if done_idx is None and n_done is None and isinstance(actions, t.Tensor) and actions.device == self.device \
                 and actions.dtype == t.float32 and actions.is_contiguous() and actions.shape == (self.n, 4):
@@ -202,12 +249,43 @@ class F16Envs:
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
+    def _step_window(self, actions, done_idx, n_done) -> StepOut:
+        """f16env_step_window: the new frame goes to position p+1 of both histories, the
+        observation is the window ending there in the history of the new parity."""
+        t = self.torch
+        if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
+                and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
+            act = actions
+        else:
+            self._act.copy_(t.as_tensor(actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
+            act = self._act
+        if tuple(act.shape) != (self.n, 4):
+            raise ValueError("actions must be (N, 4), got %s" % (tuple(act.shape),))
+        if (done_idx is None) != (n_done is None):
+            raise ValueError("done_idx and n_done go together")
+        self._need(done_idx, (self.n,), t.int32, "done_idx")
+        self._need(n_done, (1,), t.int32, "n_done")
+        s = self._stream_int()
+        p = self._p + 1
+        if p >= self.T:  # move the last K-1 frames to the front of both histories
+            check(lib().f16env_window_restart(self._h, s, self._hist_ptr[0], self._hist_ptr[1], self.T, self._p),
+                  "f16env_window_restart")
+            p = self.k - 1
+        cur = self._cur ^ 1
+        check(self._step_win_fn(self._h, s, act.data_ptr(), self._hist_ptr[cur], self._hist_ptr[cur ^ 1], self.T, p,
+                                *self._win_ptr, _ptr(done_idx), _ptr(n_done)), "f16env_step_window")
+        self._cur, self._p = cur, p
+        self.terminal_obs = self._window(1)
+        return StepOut(self._window(), self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return,
+                       self.ep_len)
+
     def step_rollout(self, seed: int, step: int, frame=None, actions=None, rewards=None, next_start=None,
                      policy_actions=None, features=None) -> StepOut:
         """One env step that also writes one rollout-buffer slot (f16env_step_rollout): the
         newest frame of the observation acted on, the actions, the rewards and the next slot's
         episode starts, with no extra launch. policy_actions None: actions drawn in-kernel
         from the sample_actions(seed, step) stream (bit-identical)."""
+        self._no_window("step_rollout")
         t = self.torch
         act = None
         if policy_actions is not None:
@@ -245,6 +323,7 @@ class F16Envs:
         (episode starts of slots 1..T-1) and last_start (N,), and leaves the env at its
         observation after the last step (self.obs). The same actions and episode starts as n_steps
         step_rollout calls; frames and rewards equal up to fp32 rounding."""
+        self._no_window("rollout_random")
         T = int(n_steps)
         n = self.n
         for name, x, shape in (("frames", frames, (T, n, F16_OBS_DIM)), ("actions", actions, (T, n, 4)),
@@ -293,7 +372,15 @@ class F16Envs:
         self.torch.cuda.current_stream(self.device).synchronize()
 
     def set_obs(self, obs):
-        self._obs[self._cur].copy_(self.torch.as_tensor(obs, dtype=self.torch.float32))
+        """Overwrite the current observation (window layout: both histories' windows, so the
+        next step continues from it)."""
+        o = self.torch.as_tensor(obs, dtype=self.torch.float32)
+        if self.window:
+            p, k = self._p, self.k
+            self._hist[0, :, p - k + 1:p + 1].copy_(o)
+            self._hist[1, :, p - k + 1:p + 1].copy_(o)
+        else:
+            self._obs[self._cur].copy_(o)
 
     def trim(self, ic):
         t = self.torch

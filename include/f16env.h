@@ -194,6 +194,31 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
                 float* rew, uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
                 double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done);
 
+/* Windowed observations: the same env step without the stack shift copy (the "state-stacking
+ * ring buffer" of BASELINE.json north_star: JSBSimEnv's `obs_buffer` deque(maxlen=K),
+ * jsbsim_gym.py:150 and its append at :235, and DummyVecEnv's stacked obs buffer,
+ * dummy_vec_env.py:56-73). The caller owns two frame histories of T frames per env,
+ * hist[b] = N x T x 15 float (T % 4 == 0, T >= 2K). The observation of a step is the window
+ *     hist_cur[k][pos-K+1 .. pos][0..15)      (a strided N x K x 15 view: strides T*15, 15, 1)
+ * with identical values to f16env_step's obs. A step writes only its new frame, at `pos` of
+ * both histories (reset lanes also fill their window), alternating hist_cur / hist_other
+ * between steps (pos advancing by one); the terminal observation of a lane that finished is
+ * the same window of hist_other (no copy; valid until the next step, like terminal_obs).
+ * The other parity's window is not written, so an observation stays valid until the step
+ * after next. When pos would reach T, f16env_window_restart moves the last K-1 frames to the
+ * front and the next step uses pos = K-1. Other arguments as f16env_step. */
+int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_cur, float* hist_other,
+                       int64_t T, int32_t pos, float* rew, uint8_t* terminated, uint8_t* truncated,
+                       double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done);
+/* f16env_reset for windowed observations: K copies of frame 0 into hist_cur's window ending at
+ * pos (mask / goals / ic as f16env_reset; jsbsim_gym.py:289-331 x N). */
+int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
+                        float* hist_cur, int64_t T, int32_t pos);
+/* Frames pos_old-K+2 .. pos_old of both histories -> 0 .. K-2 (pos_old = T-1 in practice). */
+int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, int64_t T, int32_t pos_old);
+/* Waves per SIMD the windowed step kernel of this handle is built for (1 or 2). */
+int f16env_step_window_waves_per_simd(f16env_t h);
+
 /* One env step that also fills one slot of a device rollout buffer (SURVEY.md 8f rank 1,
  * replacing the per-step stable_baselines3 RolloutBuffer.add, buffers.py:440-479, and the
  * action sampling of collect_rollouts, on_policy_algorithm.py:194-218, with no extra launch).
