@@ -240,7 +240,7 @@ __device__ __forceinline__ Seg bracket(const float (&bp)[N], const float* pairs,
 #endif
   const float2 p = reinterpret_cast<const float2*>(pairs)[i - 1];
   float f = (x - p.x) * p.y;
-  f = fminf(fmaxf(f, 0.0f), 1.0f);
+  f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
   return {i, f};
 }
 // uniform grid x0 + k*h (k = 0..N-1): same bracket semantics without a search
@@ -249,7 +249,7 @@ __device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, i
   int i = (int)floorf(u) + 1;
   i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
   float f = u - (float)(i - 1);
-  f = fminf(fmaxf(f, 0.0f), 1.0f);
+  f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
   return {i, f};
 }
 __device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (b - a) + a; }
@@ -304,7 +304,7 @@ template <int N>
 __device__ __forceinline__ float tab1_fast_end(const float (&bp)[N], const float* pairs, const float* vd, float x) {
   if (__ballot(!(x > bp[N - 2])) == 0) {  // same segment and factor as bracket() would give
     const float2 q = reinterpret_cast<const float2*>(pairs)[N - 2];
-    const float f = fminf(fmaxf((x - q.x) * q.y, 0.0f), 1.0f);
+    const float f = __builtin_amdgcn_fmed3f((x - q.x) * q.y, 0.0f, 1.0f);
     const float2 p = reinterpret_cast<const float2*>(vd)[N - 2];
     return blend(f, p.x, p.y);
   }
@@ -612,21 +612,24 @@ __device__ __forceinline__ void euler(const float* T, float& phi, float& tht, fl
 }
 
 // FCS components
-__device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// clamp as one v_med3_f32 (lo <= hi; equals min(max(x, lo), hi) for every non-NaN x)
+__device__ __forceinline__ float clipf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 __device__ __forceinline__ bool eq_roundoff(float a, float b) {
   return fabsf(a - b) <= 2.0f * 1.1920929e-07f * fmaxf(fabsf(a), fabsf(b));
 }
 // FGKinematic with two detents (single segment): rate = (d1 - d0) / t. The traverse moves
 // the output toward the (clamped) input by at most dt * rate per frame, which is the oracle's
 // "dt < |in - out| / rate ? out +- dt rate : in" as one clamp of the difference (the reached
-// value is out + (in - out), within an ulp of in). Branch-free.
+// value is out + (in - out): exactly in whenever the difference is exact, else within an ulp).
+// FGKinematic's "already there within round-off" test (oracle eq_roundoff, fp64) is not
+// restated in fp32: it would hold the output up to 2 fp32 ulps short of the input where the
+// oracle moves it onto the input. Branch-free.
 __device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float rate, float dt,
                                       bool ic) {
   in = clipf(in, d0, d1);
   if (ic) return in;  // compile-time after inlining
   const float lim = dt * rate;
-  const float moved = out + clipf(in - out, -lim, lim);
-  return eq_roundoff(in, out) ? out : moved;
+  return out + clipf(in - out, -lim, lim);
 }
 // TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350), the FGKinematic
 // while-loop of oracle kinematic() in closed form. Segment [-1, 0] has transition time 0 (the
@@ -647,19 +650,23 @@ __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic)
   const float o = seg1 ? in : (partial ? out + step : (jump2 ? in : tin));
   return eq_roundoff(in, out) ? out : o;
 }
-__device__ __forceinline__ float pidf(float in, float& itot, float& prev, float trig, float kp,
+// FGPID (rectangular integrator) with the F-16's triggers, which are switch outputs 0 / 1
+// (f16.xml:383-389, :594-604, :716-727): trigger 0 integrates, 1 holds, and the reset branch
+// (trigger < 0) cannot occur, so the trigger is passed as `integrate` (trigger == 0). KD: the
+// g-load PID has kd = 0 (no derivative term; its previous input is still tracked).
+template <bool KD = true>
+__device__ __forceinline__ float pidf(float in, float& itot, float& prev, bool integrate, float kp,
                                       float ki, float kd, float dt, bool ic) {
-  const float dval = ic ? 0.0f : (in - prev) * rcpf(dt);
-  const float delta = (!ic && fabsf(trig) < 0.000001f) ? in : 0.0f;
-  if (trig < 0.0f) itot = 0.0f;
-  itot += ki * dt * delta;
-  const float out = kp * in + itot + kd * dval;
+  if (!ic && integrate) itot += ki * dt * in;
+  float out = kp * in + itot;
+  if (KD) out += kd * (ic ? 0.0f : (in - prev) * rcpf(dt));
   prev = in;
   return out;
 }
 __device__ __forceinline__ float aero_scale(float in, float outmax) {
   // zero-centred aerosurface_scale with symmetric domain [-1,1] and range [-outmax,outmax]
-  return (in == 0.0f) ? 0.0f : in * outmax;
+  // (in == 0 -> +-0, the same value)
+  return in * outmax;
 }
 
 struct FcsOut {
@@ -698,8 +705,7 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   L.tef = kin_tef(L.tef, tef_norm, dt, ic);
   // Roll
   const float roll_err = cmd[0] - L.lx[F16L_P_AERO] * 0.31821f;
-  const float ail_trig = (qc < C.qc_vc20) ? 0.0f : 1.0f;
-  const float roll_pid = pidf(roll_err, L.pri, L.prp, ail_trig, 3.0f, 0.0005f, -0.00125f, dt, ic);
+  const float roll_pid = pidf(roll_err, L.pri, L.prp, qc < C.qc_vc20, 3.0f, 0.0005f, -0.00125f, dt, ic);
   const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
   o.da = aero_scale(roll_cmd, 0.375f);
   L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
@@ -712,15 +718,13 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
   const float ele_sched = ele_lim * tb.ele;
   const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
-  const float ele_trig = (qc < C.qc_vc5) ? 0.0f : 1.0f;
-  const float gpid = clipf(pidf(pitch_err, L.ppi, L.ppp, ele_trig, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
+  const float gpid = clipf(pidf<false>(pitch_err, L.ppi, L.ppp, qc < C.qc_vc5, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
   const float pitch_sched = clipf(ele_sched + alpha * 1.0472f + gpid, -1.0f, 1.0f);
   L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
   o.de = aero_scale(L.ele, 0.436f);
   // Yaw
   const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tb.yaw + L.lx[F16L_NPY] * 0.25f;
-  const float rud_trig = (qc < C.qc_vc10) ? 0.0f : 1.0f;
-  const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, rud_trig, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
+  const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, qc < C.qc_vc10, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
   const float yaw_sched = clipf(cmd[2] + ypid, -1.0f, 1.0f);
   L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, 2.0f / 0.4f, dt, ic);
   o.dr = aero_scale(L.rud, 0.524f);
@@ -846,7 +850,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   {
     sb7.i = 1 + ((sb13.i - 1) >> 1);
     const float2 p = reinterpret_cast<const float2*>(T + OFF_pair_beta7)[sb7.i - 1];
-    sb7.f = fminf(fmaxf((a.beta - p.x) * p.y, 0.0f), 1.0f);
+    sb7.f = __builtin_amdgcn_fmed3f((a.beta - p.x) * p.y, 0.0f, 1.0f);
   }
   float AB7[4];  // Clda, Cldr, Cnda, Cndr over (alpha, beta 7)
   {
