@@ -87,22 +87,31 @@ static constexpr float RAD2DEG_F = 57.295779513082320876798f;
 // lane state (registers) and its struct-of-arrays image in HBM
 // ------------------------------------------------------------------------------------------
 // Layout: 16-byte columns, column j of env k at c[j * n + k] (float4). A wave moves each
-// column with one coalesced dwordx4 access (1 KiB per wave-instruction): 19 wide loads and
-// stores per lane instead of 67 dword ones -- the step's store tail is issue-bound at 4 B/lane
-// (MI355X_MICROARCH.md, epilogue store tail). fp64 fields occupy two lanes of a column.
-//   C0  rI.x rI.y (f64)        C7  q0 q1 q2 q3            C14 lx1 lx2 lx3 lx4
-//   C1  rI.z vI.x (f64)        C8  wI.xyz wId.x           C15 lx5 lx6 lx7 lx8
-//   C2  vI.y vI.z (f64)        C9  wId.yz ba.xy           C16 lx9 goal.xyz
-//   C3  epa ep_ret (f64)       C10 ba.z tef ail ele       C17 last_d wind.xyz (steady)
-//   C4  dv1.xyz dv2.x          C11 rud lef sb pid_r_i     C18 step ep_count flags (i32), 0
-//   C5  dv2.yz aI.xy           C12 pid_r_p pid_p_i pid_p_p pid_y_i
-//   C6  aI.z aIp.xyz           C13 pid_y_p n1 n2 lx0      C19 gust.xyz, 0 (cfg5 gust mode only)
-enum { NCOL = 19, NCOL_ALL = 20, COL_GUST = 19 };
+// column with one coalesced dwordx4 access (1 KiB per wave-instruction): 16 wide loads and
+// stores per lane -- the step's store tail is issue-bound at 4 B/lane (MI355X_MICROARCH.md,
+// epilogue store tail). fp64 fields occupy two lanes of a column.
+//   C0  rI.x rI.y (f64)        C6  aI.z aIp.xyz           C12 pid_p_i pid_y_i pid_y_p n2'
+//   C1  rI.z vI.x (f64)        C7  q0 q1 q2 q3            C13 alpha beta mach qc      (latch)
+//   C2  vI.y vI.z (f64)        C8  wI.xyz wId.x           C14 npy npz goal.x goal.y   (latch, goal)
+//   C3  epa ep_ret (f64)       C9  wId.yz ba.y ba.z       C15 goal.z last_d' step ep_count (i32)
+//   C4  dv1.xyz dv2.x          C10 tef ail ele rud        C16 steady wind.xyz, 0  (wind kernels only)
+//   C5  dv2.yz aI.xy           C11 lef sb pid_r_i pid_r_p C17 gust.xyz, 0         (wind kernels only)
+// n2' = N2 with the augmentation flag in its sign bit (N2 >= 60 %), last_d' = last distance
+// with the FRESH flag in its sign bit (a norm, >= 0). Not stored, because a step never reads
+// them from the previous one: the latch's body rates wrt ECEF (p/q/r-aero = wI - Ti2b (0, 0,
+// w_earth), a function of q and wI) and ground speed (a function of rI, vI), recomputed at load
+// (latch_from_state) exactly as a frame computes them (the last frame of a step runs after the
+// step's final integration, so its latch is a function of the stored state); FGTurbine's N1
+// (thrust under augmethod 2 reads N2 only, and nothing observes N1); the g-load PID's previous
+// input (kd = 0); the body force's x component (only the same frame's accelerations read it).
+// get_state reports those three as 0. Handles whose lanes can carry wind (config / random-IC
+// wind, cfg5 gusts, set_state) run the wind kernels (MODE bit 1) and move C16-C17 as well.
+enum { NCOL = 16, NCOL_ALL = 18, COL_WIND = 16, COL_GUST = 17 };
 static constexpr int LANE_FLAG_AUG = 1;
 // set by every reset path, cleared by the next step: the windowed-observation step fills the
 // lane's new history window with its reset frame (f16env_step_window)
 static constexpr int LANE_FLAG_FRESH = 2;
-// persistent bytes per env moved by a step (SURVEY.md 8d "S"); +16 in gust mode
+// persistent bytes per env moved by a step (SURVEY.md 8d "S"); +32 in the wind kernels
 static constexpr int STATE_BYTES = NCOL * 16;
 static constexpr int STATE_BYTES_GUST = NCOL_ALL * 16;
 
@@ -120,8 +129,8 @@ struct Lane {
   float lx[F16L_N];
   float goal[3], last_d;
   float wind[3];  // wind the FDM sees (NED fps): steady + gust
-  float wst[3];   // steady wind (column 17); the gust-mode kernels keep it apart from
-  float gust[3];  // the cfg5 gust (column 19)
+  float wst[3];   // steady wind (column 16)
+  float gust[3];  // the cfg5 gust (column 17)
   int32_t step, ep_count, flags;
 };
 
@@ -130,9 +139,45 @@ __device__ __forceinline__ double f2d(float lo, float hi) {
 }
 __device__ __forceinline__ float dlo(double d) { return __int_as_float(__double2loint(d)); }
 __device__ __forceinline__ float dhi(double d) { return __int_as_float(__double2hiint(d)); }
+// a flag bit carried in the sign of a non-negative float
+__device__ __forceinline__ float with_sign_flag(float v, bool f) {
+  return __uint_as_float((__float_as_uint(v) & 0x7fffffffu) | (f ? 0x80000000u : 0u));
+}
+__device__ __forceinline__ bool sign_flag(float v) { return (__float_as_uint(v) >> 31) != 0; }
+__device__ __forceinline__ float without_sign_flag(float v) { return __uint_as_float(__float_as_uint(v) & 0x7fffffffu); }
+
+// body rates wrt ECEF: pqr = wI - Ti2b (0, 0, w_earth) (FGPropagate; the same expression as
+// derive's, so the recomputed latch equals the one the last frame of the previous step held)
+__device__ __forceinline__ void pqr_aero(const float* q, const float* wI, float* pqr) {
+  const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const float T2 = 2.0f * (q1 * q3 - q0 * q2);
+  const float T5 = 2.0f * (q2 * q3 + q0 * q1);
+  const float T8 = q0 * q0 - q1 * q1 - q2 * q2 + q3 * q3;
+  const float we = (float)0.00007292115;
+  pqr[0] = wI[0] - T2 * we;
+  pqr[1] = wI[1] - T5 * we;
+  pqr[2] = wI[2] - T8 * we;
+}
+// ground speed (FGAuxiliary Vground): horizontal part of the velocity wrt the rotating Earth,
+// |v|^2 - (v . r_hat)^2 with r_hat the geocentric up (the local frame's down axis is -r_hat).
+// Frames compute it the same way from their fp32 quantities (ground_speed below).
+__device__ __forceinline__ float ground_speed(float vx, float vy, float vz, float rx, float ry, float rz) {
+  const float vv = vx * vx + vy * vy + vz * vz;
+  const float vr = vx * rx + vy * ry + vz * rz;
+  const float rr = rx * rx + ry * ry + rz * rz;
+  return __builtin_amdgcn_sqrtf(fmaxf(vv - vr * vr * __builtin_amdgcn_rcpf(rr), 0.0f));
+}
+__device__ __forceinline__ void latch_from_state(Lane& L) {
+  float pqr[3];
+  pqr_aero(L.q, L.wI, pqr);
+  L.lx[F16L_P_AERO] = pqr[0]; L.lx[F16L_Q_AERO] = pqr[1]; L.lx[F16L_R_AERO] = pqr[2];
+  const double w = 0.00007292115;
+  L.lx[F16L_VG_FPS] = ground_speed((float)(L.vI[0] + w * L.rI[1]), (float)(L.vI[1] - w * L.rI[0]), (float)L.vI[2],
+                                   (float)L.rI[0], (float)L.rI[1], (float)L.rI[2]);
+}
 
 template <bool GUST>
-__device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 g, Lane& L) {
+__device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, float4 g, Lane& L) {
   L.rI[0] = f2d(c[0].x, c[0].y); L.rI[1] = f2d(c[0].z, c[0].w);
   L.rI[2] = f2d(c[1].x, c[1].y); L.vI[0] = f2d(c[1].z, c[1].w);
   L.vI[1] = f2d(c[2].x, c[2].y); L.vI[2] = f2d(c[2].z, c[2].w);
@@ -142,19 +187,23 @@ __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 g, L
   L.aI[2] = c[6].x; L.aIp[0] = c[6].y; L.aIp[1] = c[6].z; L.aIp[2] = c[6].w;
   L.q[0] = c[7].x; L.q[1] = c[7].y; L.q[2] = c[7].z; L.q[3] = c[7].w;
   L.wI[0] = c[8].x; L.wI[1] = c[8].y; L.wI[2] = c[8].z; L.wId[0] = c[8].w;
-  L.wId[1] = c[9].x; L.wId[2] = c[9].y; L.ba[0] = c[9].z; L.ba[1] = c[9].w;
-  L.ba[2] = c[10].x; L.tef = c[10].y; L.ail = c[10].z; L.ele = c[10].w;
-  L.rud = c[11].x; L.lef = c[11].y; L.sb = c[11].z; L.pri = c[11].w;
-  L.prp = c[12].x; L.ppi = c[12].y; L.ppp = c[12].z; L.pyi = c[12].w;
-  L.pyp = c[13].x; L.n1 = c[13].y; L.n2 = c[13].z; L.lx[0] = c[13].w;
-  L.lx[1] = c[14].x; L.lx[2] = c[14].y; L.lx[3] = c[14].z; L.lx[4] = c[14].w;
-  L.lx[5] = c[15].x; L.lx[6] = c[15].y; L.lx[7] = c[15].z; L.lx[8] = c[15].w;
-  L.lx[9] = c[16].x; L.goal[0] = c[16].y; L.goal[1] = c[16].z; L.goal[2] = c[16].w;
-  L.last_d = c[17].x; L.wst[0] = c[17].y; L.wst[1] = c[17].z; L.wst[2] = c[17].w;
-  L.step = __float_as_int(c[18].x); L.ep_count = __float_as_int(c[18].y); L.flags = __float_as_int(c[18].z);
-  L.gust[0] = g.x; L.gust[1] = g.y; L.gust[2] = g.z;
+  L.wId[1] = c[9].x; L.wId[2] = c[9].y; L.ba[0] = 0.0f; L.ba[1] = c[9].z; L.ba[2] = c[9].w;
+  L.tef = c[10].x; L.ail = c[10].y; L.ele = c[10].z; L.rud = c[10].w;
+  L.lef = c[11].x; L.sb = c[11].y; L.pri = c[11].z; L.prp = c[11].w;
+  L.ppi = c[12].x; L.pyi = c[12].y; L.pyp = c[12].z; L.ppp = 0.0f;
+  L.n2 = without_sign_flag(c[12].w); L.n1 = 0.0f;
+  L.lx[F16L_ALPHA] = c[13].x; L.lx[F16L_BETA] = c[13].y; L.lx[F16L_MACH] = c[13].z; L.lx[F16L_VC_KTS] = c[13].w;
+  L.lx[F16L_NPY] = c[14].x; L.lx[F16L_NPZ] = c[14].y; L.goal[0] = c[14].z; L.goal[1] = c[14].w;
+  L.goal[2] = c[15].x; L.last_d = without_sign_flag(c[15].y);
+  L.step = __float_as_int(c[15].z); L.ep_count = __float_as_int(c[15].w);
+  L.flags = (sign_flag(c[12].w) ? LANE_FLAG_AUG : 0) | (sign_flag(c[15].y) ? LANE_FLAG_FRESH : 0);
+  latch_from_state(L);
 #pragma unroll
-  for (int j = 0; j < 3; ++j) L.wind[j] = GUST ? L.wst[j] + L.gust[j] : L.wst[j];
+  for (int j = 0; j < 3; ++j) {
+    L.wst[j] = GUST ? (&w.x)[j] : 0.0f;
+    L.gust[j] = GUST ? (&g.x)[j] : 0.0f;
+    L.wind[j] = L.wst[j] + L.gust[j];
+  }
 }
 template <bool GUST = false>
 __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
@@ -164,17 +213,22 @@ __device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
   const float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n) c[j] = *p;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (GUST) g = *p;
-  lane_unpack<GUST>(c, g, L);
+  float4 w = make_float4(0.f, 0.f, 0.f, 0.f), g = w;
+  if (GUST) {
+    w = *p;
+    g = *(p + n);
+  }
+  lane_unpack<GUST>(c, w, g, L);
 }
 // the one-env IC template staged in LDS (columns contiguous): no vector-memory traffic, so
-// the reset of a finished lane adds no vmcnt dependency to the step's store tail
+// the reset of a finished lane adds no vmcnt dependency to the step's store tail (MODE 0:
+// the template carries no wind)
 __device__ __forceinline__ void lane_load_lds(const float4* cols, Lane& L) {
   float4 c[NCOL];
 #pragma unroll
   for (int j = 0; j < NCOL; ++j) c[j] = cols[j];
-  lane_unpack<false>(c, make_float4(0.f, 0.f, 0.f, 0.f), L);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  lane_unpack<false>(c, z, z, L);
 }
 
 template <bool GUST = false>
@@ -190,21 +244,21 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   c[6] = make_float4(L.aI[2], L.aIp[0], L.aIp[1], L.aIp[2]);
   c[7] = make_float4(L.q[0], L.q[1], L.q[2], L.q[3]);
   c[8] = make_float4(L.wI[0], L.wI[1], L.wI[2], L.wId[0]);
-  c[9] = make_float4(L.wId[1], L.wId[2], L.ba[0], L.ba[1]);
-  c[10] = make_float4(L.ba[2], L.tef, L.ail, L.ele);
-  c[11] = make_float4(L.rud, L.lef, L.sb, L.pri);
-  c[12] = make_float4(L.prp, L.ppi, L.ppp, L.pyi);
-  c[13] = make_float4(L.pyp, L.n1, L.n2, L.lx[0]);
-  c[14] = make_float4(L.lx[1], L.lx[2], L.lx[3], L.lx[4]);
-  c[15] = make_float4(L.lx[5], L.lx[6], L.lx[7], L.lx[8]);
-  c[16] = make_float4(L.lx[9], L.goal[0], L.goal[1], L.goal[2]);
-  c[17] = GUST ? make_float4(L.last_d, L.wst[0], L.wst[1], L.wst[2])
-               : make_float4(L.last_d, L.wind[0], L.wind[1], L.wind[2]);
-  c[18] = make_float4(__int_as_float(L.step), __int_as_float(L.ep_count), __int_as_float(L.flags), 0.0f);
+  c[9] = make_float4(L.wId[1], L.wId[2], L.ba[1], L.ba[2]);
+  c[10] = make_float4(L.tef, L.ail, L.ele, L.rud);
+  c[11] = make_float4(L.lef, L.sb, L.pri, L.prp);
+  c[12] = make_float4(L.ppi, L.pyi, L.pyp, with_sign_flag(L.n2, (L.flags & LANE_FLAG_AUG) != 0));
+  c[13] = make_float4(L.lx[F16L_ALPHA], L.lx[F16L_BETA], L.lx[F16L_MACH], L.lx[F16L_VC_KTS]);
+  c[14] = make_float4(L.lx[F16L_NPY], L.lx[F16L_NPZ], L.goal[0], L.goal[1]);
+  c[15] = make_float4(L.goal[2], with_sign_flag(L.last_d, (L.flags & LANE_FLAG_FRESH) != 0),
+                      __int_as_float(L.step), __int_as_float(L.ep_count));
   float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n) *p = c[j];
-  if (GUST) *p = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
+  if (GUST) {
+    *p = make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f);
+    *(p + n) = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -437,7 +491,8 @@ __device__ __forceinline__ float qc_from_vcas(double vc_kts, const ModelConsts& 
 // ------------------------------------------------------------------------------------------
 struct Derived {
   float Ti2b[9], Tec2b[9], Tl2b[9];
-  float uvw[3], pqr[3], vned[3];
+  float uvw[3], pqr[3];
+  float vg;         // ground speed (latch_from_state's expression)
   float gE[3];      // J2 gravity, ECEF
   double h_ft;
 };
@@ -572,11 +627,8 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
                        (float)L.vI[2]};
   mvec(d.Ti2b, vr, d.uvw);
   // vPQR = vPQRi - Ti2b * (0,0,w)
-  const float we = (float)OMEGA_E;
-  d.pqr[0] = L.wI[0] - d.Ti2b[2] * we;
-  d.pqr[1] = L.wI[1] - d.Ti2b[5] * we;
-  d.pqr[2] = L.wI[2] - d.Ti2b[8] * we;
-  mtvec(d.Tl2b, d.uvw, d.vned);
+  pqr_aero(L.q, L.wI, d.pqr);
+  d.vg = ground_speed(vr[0], vr[1], vr[2], (float)L.rI[0], (float)L.rI[1], (float)L.rI[2]);
   // J2 gravity (FGInertial::GetGravityJ2), ECEF
   const float adivr = (float)WGS_A * inv_r;
   const float pre = 1.5f * (float)J2_E * adivr * adivr;
@@ -917,7 +969,9 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 // scheduler cannot hoist the calibrated-airspeed chain into the aerodynamics' live range
 // (scratch 168 -> 152 B; 131 072 envs 39.4 -> 38.1 us, 65 536 envs unchanged: only the
 // 256-register build takes it)
-template <bool LOWREG = false>
+// WIND: the lane may carry wind (the wind kernels, IC passes); false skips the air-relative
+// velocity's wind term (reference task: no wind, jsbsim_gym.py never enables FGWinds).
+template <bool LOWREG = false, bool WIND = true>
 __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se, const AltRef& A,
                                       const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
   const float dt = (float)C.dt;
@@ -967,8 +1021,8 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   derive(L, ce, se, A, d);
   F16_STAMP(stamps, ST_DERIVE);
   // -- Auxiliary, wind-axis part (needs no atmosphere) --
-  float wb[3];
-  mvec(d.Tl2b, L.wind, wb);
+  float wb[3] = {0.0f, 0.0f, 0.0f};
+  if (WIND) mvec(d.Tl2b, L.wind, wb);
   const float ua = d.uvw[0] - wb[0], va = d.uvw[1] - wb[1], wa = d.uvw[2] - wb[2];
   const float muw = ua * ua + wa * wa;
   const float vt = fsqrt(muw + va * va);
@@ -983,7 +1037,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const float cb_ = moving ? suw * ivt : 1.0f, sb_ = moving ? va * ivt : 0.0f;
   const float inv2v = (vt != 0.0f) ? 0.5f * ivt : 0.0f;
   const float bi2vel = B_W * inv2v, ci2vel = CBAR * inv2v;
-  const float vg = fsqrt(d.vned[0] * d.vned[0] + d.vned[1] * d.vned[1]);
+  const float vg = d.vg;
   // pilot-station load factors from the PREVIOUS frame's accelerations (FGAuxiliary runs
   // before FGAccelerations)
   float t1[3], t2[3], t3[3];

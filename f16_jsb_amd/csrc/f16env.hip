@@ -338,7 +338,7 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
     }
     apply_ic(L, ic, T, C);
   } else {
-    lane_load(tmpl, 0, L);
+    lane_load<true>(tmpl, 0, L);  // the config IC (its wind included: MODE 0 handles have none)
   }
   if (goal) {
     L.goal[0] = goal[0]; L.goal[1] = goal[1]; L.goal[2] = goal[2];
@@ -604,7 +604,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     double ce, se;
     earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
-    for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
     make_frame(L, ce, se, A, f);                              // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261), PositionReward (:493-507)
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
     double ce, se;
     earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);
-    for (int s = 0; s < a.E.down_sample; ++s) frame(L, cmd, ce, se, A, sT, a.C, false);  // :225-232
+    for (int s = 0; s < a.E.down_sample; ++s) frame<false, false>(L, cmd, ce, se, A, sT, a.C, false);  // :225-232
     float f[F16_OBS_DIM];
     make_frame(L, ce, se, A, f);                              // :234
     float r32;
@@ -1084,7 +1084,7 @@ __global__ void f16_ic_kernel(SoA dst, const double* ic, ModelConsts C) {
   apply_ic(L, ic, sT, C);
   L.ep_ret = 0.0; L.step = 0; L.ep_count = 0; L.last_d = 0.0f;
   L.goal[0] = L.goal[1] = L.goal[2] = 0.0f;
-  lane_store(dst, 0, L);
+  lane_store<true>(dst, 0, L);  // with the config IC's wind columns (read by wind-kernel resets)
   // frame 0 of the template (goal excluded): what every template auto-reset would evaluate
   float f[F16_OBS_DIM];
   make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f);
@@ -1120,7 +1120,7 @@ __global__ void f16_get_state_kernel(SoA s, double* c, ModelConsts C) {
   o[F16C_EP_COUNT] = (double)(uint32_t)L.ep_count;
 }
 
-__global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C) {
+__global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int* wind_any) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= s.n) return;
   Lane L;
@@ -1148,6 +1148,10 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C) {
   L.last_d = (float)o[F16C_LAST_D]; L.step = (int32_t)o[F16C_STEP]; L.ep_ret = o[F16C_EP_RET];
   L.ep_count = (int32_t)(uint32_t)o[F16C_EP_COUNT];
   lane_store<true>(s, k, L);
+  // a lane with wind needs the wind kernels (f16env_set_state switches the handle)
+  bool w = false;
+  for (int j = 0; j < 3; ++j) w = w || L.wst[j] != 0.0f || L.gust[j] != 0.0f;
+  if (w) atomicOr(wind_any, 1);
 }
 
 // Trim: Newton on (alpha, elevator cmd, throttle cmd), mirrors oracle trim_one()
@@ -1360,8 +1364,10 @@ struct f16env {
   void* tmem;      // template SoA (n = 1)
   double* ic_dev;  // default IC, RANDOM_IC box lo, hi (3 x F16_IC_N)
   int32_t* done_buf;  // deferred modes: own done list (N) + count, when the caller gives none
-  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine counter (device, 8 B)
-  int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 GUSTS
+  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine counter (device, 8 B) + a
+                                  // scratch word (set_state's wind detection)
+  int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 wind (GUSTS, or lanes with
+                      // steady wind: config / random-IC box / set_state)
   int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
   int win_occ;        // the same for the windowed-observation step kernel
   SoA soa, tmpl;
@@ -1465,6 +1471,9 @@ static EnvArgs env_args(const f16env* h) {
   E.gust_a = (float)ga;
   E.gust_b = (float)(h->cfg.gust_sigma_fps * sqrt(1.0 - ga * ga));
   E.gust_sigma = (float)h->cfg.gust_sigma_fps;
+  if (!(h->cfg.flags & F16_FLAG_GUSTS)) {  // wind kernels without gusts: the gust term holds still
+    E.gust_a = 1.0f; E.gust_b = 0.0f; E.gust_sigma = 0.0f;
+  }
   return E;
 }
 
@@ -1525,16 +1534,20 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   if (e != hipSuccess) { delete h; return set_err(-3, "hipMalloc(state) failed"); }
   hipMemset(h->mem, 0, h->bytes);
   soa_carve(h->mem, cfg->n_envs, h->soa);
-  h->mode = ((cfg->flags & F16_FLAG_RANDOM_IC) ? 1 : 0) | ((cfg->flags & F16_FLAG_GUSTS) ? 2 : 0);
+  bool wind = false;  // can any lane carry wind? (then the wind kernels: MODE bit 1)
+  for (int j = F16_IC_WIND_N_FPS; j <= F16_IC_WIND_D_FPS; ++j)
+    wind = wind || cfg->ic[j] != 0.0 ||
+           ((cfg->flags & F16_FLAG_RANDOM_IC) && (cfg->ic_lo[j] != 0.0 || cfg->ic_hi[j] != 0.0));
+  h->mode = ((cfg->flags & F16_FLAG_RANDOM_IC) ? 1 : 0) | (((cfg->flags & F16_FLAG_GUSTS) || wind) ? 2 : 0);
   h->done_buf = nullptr;
   if (hipMalloc(&h->tmem, (size_t)TMPL_COLS * 16) != hipSuccess ||
       hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||
-      (h->mode && hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 1)) != hipSuccess)) {
+      hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 1)) != hipSuccess) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
     return set_err(-3, "hipMalloc(template) failed");
   }
   soa_carve(h->tmem, 1, h->tmpl);
-  if (hipMalloc((void**)&h->nonfinite, sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMalloc((void**)&h->nonfinite, 2 * sizeof(unsigned long long)) != hipSuccess) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
     return set_err(-3, "hipMalloc(counter) failed");
   }
@@ -1861,8 +1874,15 @@ int f16env_get_state(f16env_t h, void* stream, double* canon) {
 
 int f16env_set_state(f16env_t h, void* stream, const double* canon) {
   if (!h || !canon) return set_err(-1, "null argument");
-  hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa, canon, h->C);
+  hipStream_t st = (hipStream_t)stream;
+  int* wind_any = reinterpret_cast<int*>(h->nonfinite + 1);
+  HIPCHK(hipMemsetAsync(wind_any, 0, sizeof(int), st));
+  hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, st, h->soa, canon, h->C, wind_any);
   HIPCHK(hipGetLastError());
+  int w = 0;
+  HIPCHK(hipMemcpyAsync(&w, wind_any, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (w) h->mode |= 2;  // lanes with wind: the wind kernels from now on
   return 0;
 }
 
@@ -1921,6 +1941,7 @@ int f16env_poses(void* stream, int64_t n, const float* frames, int64_t frame_str
 
 const char* f16env_step_kernel_name(void) { return "f16_step_kernel"; }
 int f16env_step_waves_per_simd(f16env_t h) { return h ? h->occ : 0; }
+int f16env_step_mode(f16env_t h) { return h ? h->mode : -1; }
 int f16env_step_variant(f16env_t h) { return h ? (h->gt ? 2 : (h->occ == 2 ? 1 : 0)) : -1; }
 
 double f16env_algorithmic_bytes_per_env_step(int stack_k) {

@@ -160,7 +160,7 @@ class F16Envs:
 
     @property
     def step_kernel_name(self) -> str:
-        mode = (1 if self.cfg.flags & F16_FLAG_RANDOM_IC else 0) | (2 if self.cfg.flags & F16_FLAG_GUSTS else 0)
+        mode = int(lib().f16env_step_mode(self._h))
         if self.window:
             return "f16_step_win_kernel<%d, %d>" % (mode, self.waves_per_simd)
         variant = int(lib().f16env_step_variant(self._h))

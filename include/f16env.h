@@ -78,7 +78,9 @@ enum f16_canon_index {
   F16C_Q = 18,       /* 18-21 attitude quaternion ECI->body (q0 q1 q2 q3)              */
   F16C_WI = 22,      /* 22-24 body rates wrt ECI, body axes (vPQRi)                    */
   F16C_WID = 25,     /* 25-27 latest vPQRidot                                          */
-  F16C_BA = 28,      /* 28-30 latest body specific-force acceleration (vBodyAccel)     */
+  F16C_BA = 28,      /* 28-30 latest body specific-force acceleration (vBodyAccel); the  */
+                     /* HIP path carries y, z (read by the next frame's pilot load      */
+                     /* factors) and reports x as 0                                     */
   F16C_EPA_C = 31,   /* cos / sin of the Earth position angle                          */
   F16C_EPA_S = 32,
   F16C_TEF = 33,     /* fcs/tef-control            (kinematic, f16.xml:334-350)        */
@@ -89,11 +91,14 @@ enum f16_canon_index {
   F16C_SB = 38,      /* fcs/speedbrake-pos-deg     (kinematic, f16.xml:909-922)        */
   F16C_PID_R_I = 39, /* roll-rate-pid  (f16.xml:383-389): integrator, previous input   */
   F16C_PID_R_P = 40,
-  F16C_PID_P_I = 41, /* g-load-pid     (f16.xml:594-604)                               */
+  F16C_PID_P_I = 41, /* g-load-pid     (f16.xml:594-604); kd = 0, so the HIP path does   */
+                     /* not carry its previous input (PID_P_P reported as 0)            */
   F16C_PID_P_P = 42,
   F16C_PID_Y_I = 43, /* yaw-load-pid   (f16.xml:716-727)                               */
   F16C_PID_Y_P = 44,
-  F16C_N1 = 45,      /* FGTurbine N1, N2 (%), augmentation flag                         */
+  F16C_N1 = 45,      /* FGTurbine N1, N2 (%), augmentation flag. The HIP path does not   */
+                     /* carry N1 (thrust under augmethod 2 reads N2 only; nothing        */
+                     /* observes N1): reported as 0, ignored by set_state                */
   F16C_N2 = 46,
   F16C_AUG = 47,
   F16C_LX = 48,      /* 48-57 auxiliary latch read by the next frame's FCS:             */
@@ -168,7 +173,12 @@ int f16env_config_cfg5(f16env_config* cfg);
 int f16env_create(const f16env_config* cfg, int device, f16env_t* out);
 int f16env_destroy(f16env_t h);
 
-/* Bytes of device state held by the handle / persistent bytes per env (roofline S). */
+/* Step kernel family of the handle: bit 0 random IC, bit 1 wind (cfg5 gusts, or lanes that
+ * can carry steady wind: config IC / random-IC box wind, or set by f16env_set_state). */
+int f16env_step_mode(f16env_t h);
+
+/* Bytes of device state held by the handle / persistent bytes per env (roofline S: 256 B,
+ * +32 B for the wind kernels' steady-wind and gust columns). */
 size_t f16env_state_bytes(f16env_t h);
 int f16env_state_bytes_per_env(void);
 
@@ -266,7 +276,9 @@ int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step
 /* Lanes quarantined by F16_FLAG_NAN_GUARD since create (waits for `stream`). */
 int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);
 
-/* Canonical state export/import: canon is N x F16C_N double (device). */
+/* Canonical state export/import: canon is N x F16C_N double (device). The latch's p/q/r-aero
+ * and ground speed are recomputed from the state on import (they are functions of it);
+ * set_state waits for `stream` (it reads back whether any lane carries wind). */
 int f16env_get_state(f16env_t h, void* stream, double* canon);
 int f16env_set_state(f16env_t h, void* stream, const double* canon);
 
