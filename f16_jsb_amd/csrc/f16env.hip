@@ -1037,6 +1037,7 @@ struct ResetArgs {
   const double* ic;
   float* obs;       // row addressing as ResetDoneArgs
   int64_t obs_row, obs_off;
+  int* wind_any;    // per-lane IC given: set if a lane got wind (the handle needs the wind kernels)
   EnvArgs E;
   ModelConsts C;
 };
@@ -1055,6 +1056,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   if (g && isnan(g[0])) g = nullptr;
   lane_reset(L, a.tmpl, a.ic ? a.ic + (int64_t)F16_IC_N * k : nullptr, g, a.E, k, sT, a.C, f0);
   lane_store<true>(a.s, k, L);
+  if (a.wind_any && (L.wst[0] != 0.0f || L.wst[1] != 0.0f || L.wst[2] != 0.0f)) atomicOr(a.wind_any, 1);
   if (a.obs) {
     float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
@@ -1657,6 +1659,26 @@ int f16env_state_bytes_per_env(void) { return STATE_BYTES; }
 
 static inline unsigned nblocks(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
+// reset launch shared by f16env_reset / f16env_reset_window. A per-lane IC may carry wind:
+// then the handle reads back (waits for the stream) whether any lane got some, and switches to
+// the wind kernels if so (the caller's IC is not hot-path).
+static int reset_launch(f16env_t h, hipStream_t st, ResetArgs& a) {
+  a.wind_any = nullptr;
+  if (a.ic && !(h->mode & 2)) {
+    a.wind_any = reinterpret_cast<int*>(h->nonfinite + 1);
+    HIPCHK(hipMemsetAsync(a.wind_any, 0, sizeof(int), st));
+  }
+  hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, st, a);
+  HIPCHK(hipGetLastError());
+  if (a.wind_any) {
+    int w = 0;
+    HIPCHK(hipMemcpyAsync(&w, a.wind_any, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (w) h->mode |= 2;
+  }
+  return 0;
+}
+
 int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic, float* obs) {
   if (!h) return set_err(-1, "null handle");
   ResetArgs a;
@@ -1664,9 +1686,7 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   a.obs_row = (int64_t)h->cfg.stack_k * F16_OBS_DIM; a.obs_off = 0;
   a.E = env_args(h);
   a.C = h->C;
-  hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
+  return reset_launch(h, (hipStream_t)stream, a);
 }
 
 static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
@@ -1803,9 +1823,7 @@ int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const flo
   a.obs_row = T * F16_OBS_DIM; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * F16_OBS_DIM;
   a.E = env_args(h);
   a.C = h->C;
-  hipLaunchKernelGGL(f16_reset_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), 0, (hipStream_t)stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
+  return reset_launch(h, (hipStream_t)stream, a);
 }
 
 int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, int64_t T, int32_t pos_old) {

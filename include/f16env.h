@@ -186,7 +186,9 @@ int f16env_state_bytes_per_env(void);
  *   goals: N x 3 float (x, y, alt in m) or NULL -> device Philox goal RNG; a row whose x is
  *          NaN also takes the device goal (seeded and unseeded lanes in one call)
  *   ic:    N x F16_IC_N double or NULL -> the config's default IC (template copy)
- *   obs:   N x K x 15 float; rows of reset lanes are written (K copies of frame 0). */
+ *   obs:   N x K x 15 float; rows of reset lanes are written (K copies of frame 0).
+ * With a per-lane ic on a handle without the wind kernels the call waits for `stream` to read
+ * back whether any lane got wind (and switches the handle to the wind kernels if so). */
 int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goals,
                  const double* ic, float* obs);
 
