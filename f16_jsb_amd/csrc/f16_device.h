@@ -58,9 +58,6 @@ __device__ __forceinline__ unsigned long long memtime() {
 // oracle's init_consts(), in double, then stored in the kernel argument block)
 // ------------------------------------------------------------------------------------------
 struct ModelConsts {
-  float inv_mass;            // 1/slug
-  float J[9], Jinv[9];       // body inertia, slug ft^2
-  float rp[3], eye[3], eng[3];  // AERORP / EYEPOINT / thruster rel. CG (body ft)
   float inv_gref;            // 1 / (GM/a^2)
   float rho_sl, a_sl, p_sl;  // US-76 sea level (slug/ft3, ft/s, psf)
   float inv_rho_sl, inv_p_sl;
@@ -69,6 +66,64 @@ struct ModelConsts {
   double cos_dE, sin_dE;     // rotation of the Earth per frame (omega * dt)
   double dt;
 };
+
+// Mass properties (FGMassBalance with the tanks pinned to 1000 lb before every run(),
+// jsbsim_gym.py:227-228, so constant): oracle init_consts() restated as a constant expression
+// (f16.xml:37-83 empty weight / CG / inertia, :245-300 pilot and tanks), evaluated in double at
+// compile time and used by the frames as fp32 literals -- the zero products of inertia (the
+// airframe is symmetric, Ixy = Iyz = 0) and the zero lateral offsets of the eye point, the
+// aero reference point and the thruster then cost no instructions.
+struct MassProps {
+  float inv_mass;                 // 1/slug
+  float J[9], Jinv[9];            // body inertia about the CG, slug ft^2
+  float rp[3], eye[3], eng[3];    // AERORP / EYEPOINT / thruster relative to the CG (body ft)
+};
+constexpr MassProps f16_mass_props() {
+  const double SLUG2LB = 32.174049, IN2FT = 1.0 / 12.0;
+  const double empty = 17400.0, cg_e[3] = {-193.0, 0.0, -5.1};
+  const double pilot = 230.0, pilot_loc[3] = {-336.2, 0.0, 0.0};
+  const double tank_w[4] = {1000.0, 1000.0, 0.0, 0.0};
+  const double tank_loc[4][3] = {{-174.4, 65.0, 5.0}, {-174.4, -65.0, 5.0}, {-174.4, 65.0, -15.0}, {-174.4, -65.0, -15.0}};
+  double W = empty + pilot, m[3] = {0.0, 0.0, 0.0}, cg[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < 3; ++i) m[i] = empty * cg_e[i] + pilot * pilot_loc[i];
+  for (int t = 0; t < 4; ++t) {
+    W += tank_w[t];
+    for (int i = 0; i < 3; ++i) m[i] += tank_w[t] * tank_loc[t][i];
+  }
+  for (int i = 0; i < 3; ++i) cg[i] = m[i] / W;
+  const double mass = W / SLUG2LB;
+  double J[9] = {9496, 0, -982, 0, 55814, 0, -982, 0, 63100};
+  // point masses (pilot, tanks) at their structural locations -> body axes about the CG
+  const double* locs[5] = {pilot_loc, tank_loc[0], tank_loc[1], tank_loc[2], tank_loc[3]};
+  const double ws[5] = {pilot, tank_w[0], tank_w[1], tank_w[2], tank_w[3]};
+  for (int p = 0; p < 5; ++p) {
+    const double* r = locs[p];
+    const double v[3] = {IN2FT * (cg[0] - r[0]), IN2FT * (r[1] - cg[1]), IN2FT * (cg[2] - r[2])};
+    const double mm = ws[p] / SLUG2LB;
+    const double sv[3] = {mm * v[0], mm * v[1], mm * v[2]};
+    const double xx = sv[0] * v[0], yy = sv[1] * v[1], zz = sv[2] * v[2];
+    const double xy = -sv[0] * v[1], xz = -sv[0] * v[2], yz = -sv[1] * v[2];
+    J[0] += yy + zz; J[1] += xy; J[2] += xz; J[3] += xy; J[4] += xx + zz; J[5] += yz;
+    J[6] += xz; J[7] += yz; J[8] += xx + yy;
+  }
+  const double a = J[0], b = J[1], c = J[2], d = J[3], e = J[4], f = J[5], g = J[6], h = J[7], k = J[8];
+  const double A = e * k - f * h, B = -(d * k - f * g), Cc = d * h - e * g;
+  const double det = a * A + b * B + c * Cc, r = 1.0 / det;
+  const double Ji[9] = {A * r, -(b * k - c * h) * r, (b * f - c * e) * r, B * r, (a * k - c * g) * r,
+                        -(a * f - c * d) * r, Cc * r, -(a * h - b * g) * r, (a * e - b * d) * r};
+  MassProps P{};
+  P.inv_mass = (float)(1.0 / mass);
+  for (int i = 0; i < 9; ++i) { P.J[i] = (float)J[i]; P.Jinv[i] = (float)Ji[i]; }
+  const double aerorp[3] = {-189.5, 0.0, 3.9}, eye[3] = {-336.2, 0.0, 29.5}, eng[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < 3; ++i) {
+    const double s = (i == 1) ? 1.0 : -1.0;  // structural -> body: x and z flip, y keeps its sign
+    P.rp[i] = (float)(IN2FT * s * (aerorp[i] - cg[i]));
+    P.eye[i] = (float)(IN2FT * s * (eye[i] - cg[i]));
+    P.eng[i] = (float)(IN2FT * s * (eng[i] - cg[i]));
+  }
+  return P;
+}
+static constexpr MassProps MP = f16_mass_props();
 
 static constexpr double WGS_A = 20925646.32546;
 static constexpr double WGS_B = 20855486.5951;
@@ -490,10 +545,10 @@ __device__ __forceinline__ float qc_from_vcas(double vc_kts, const ModelConsts& 
 // frames
 // ------------------------------------------------------------------------------------------
 struct Derived {
-  float Ti2b[9], Tec2b[9], Tl2b[9];
+  float Ti2b[9], Tl2b[9];
   float uvw[3], pqr[3];
   float vg;         // ground speed (latch_from_state's expression)
-  float gE[3];      // J2 gravity, ECEF
+  float gI[3];      // J2 gravity in ECI axes
   double h_ft;
 };
 
@@ -532,6 +587,36 @@ __device__ __forceinline__ void crossf(const float* a, const float* b, float* o)
   const float y = a[2] * b[0] - a[0] * b[2];
   const float z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
+}
+
+// Products with a compile-time constant matrix / vector (MP): the terms whose constant is
+// zero are left out at compile time (an IEEE compiler may not drop x * 0.0f by itself).
+__device__ __forceinline__ float dot3c(const float* m, const float* v) {
+  float s = 0.0f;
+  bool any = false;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (m[j] != 0.0f) {
+      s = any ? __builtin_fmaf(m[j], v[j], s) : m[j] * v[j];
+      any = true;
+    }
+  return s;
+}
+__device__ __forceinline__ void mvec_c(const float* M, const float* v, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = dot3c(M + 3 * i, v);
+}
+// a x b and b x a with a compile-time constant a
+__device__ __forceinline__ void cross_c(const float* a, const float* b, float* o) {
+  auto term = [](float ai, float bj, float ak, float bk) {  // ai bj - ak bk
+    if (ai == 0.0f && ak == 0.0f) return 0.0f;
+    if (ak == 0.0f) return ai * bj;
+    if (ai == 0.0f) return -ak * bk;
+    return __builtin_fmaf(ai, bj, -ak * bk);
+  };
+  o[0] = term(a[1], b[2], a[2], b[1]);
+  o[1] = term(a[2], b[0], a[0], b[2]);
+  o[2] = term(a[0], b[1], a[1], b[0]);
 }
 
 // Geodetic altitude from ECEF (Fukushima 2006, one Halley step; FGLocation), fp64, plus
@@ -584,40 +669,36 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
     const float dx = (float)(xE - A.r0[0]), dy = (float)(yE - A.r0[1]), dz = (float)(zE - A.r0[2]);
     d.h_ft = A.h0 + (double)(A.n[0] * dx + A.n[1] * dy + A.n[2] * dz);
   }
-  // direction cosines only need fp32
-  const float xf = (float)xE, yf = (float)yE, zf = (float)zE;
-  const float rxyf = fsqrt(xf * xf + yf * yf);
+  // The local NED frame (FGLocation's, geocentric) and J2 gravity (FGInertial::GetGravityJ2)
+  // are symmetric about the Earth's axis, so they are evaluated in ECI axes from the ECI
+  // position: the same rotations as ECEF -> local composed with Ti2b * Tec2i, without
+  // forming Tec2b (FGPropagate's Tec2b and Tec2l products). fp32 direction cosines.
+  const float xi = (float)L.rI[0], yi = (float)L.rI[1], zf = (float)zE;
+  const float rxyf = fsqrt(xi * xi + yi * yi);
   const float rf = fsqrt(rxyf * rxyf + zf * zf);
   const float inv_r = rcpf(rf);
   const float slat = zf * inv_r, clat = rxyf * inv_r;
-  float slon = 0.0f, clon = 1.0f;
+  float slon = 0.0f, clon = 1.0f;  // of the ECI position (Earth longitude + Earth angle)
   if (rxyf != 0.0f) {
     const float inv = rcpf(rxyf);
-    slon = yf * inv;
-    clon = xf * inv;
+    slon = yi * inv;
+    clon = xi * inv;
   }
-  if (lat_gc_out) {
-    *lat_gc_out = atan2f(zf, rxyf);
-    *lon_out = (rxyf == 0.0f) ? 0.0f : atan2f(yf, xf);
+  if (lat_gc_out) {  // geocentric latitude / ECEF longitude for the observation
+    const float xf = (float)xE, yf = (float)yE;
+    const float rxyE = fsqrt(xf * xf + yf * yf);
+    *lat_gc_out = atan2f(zf, rxyE);
+    *lon_out = (rxyE == 0.0f) ? 0.0f : atan2f(yf, xf);
   }
-  // Tec2l (geocentric, FGLocation)
+  // Ti2l rows (north, east, down) in ECI
   const float L0 = -clon * slat, L1 = -slon * slat, L2 = clat;
   const float L3 = -slon, L4 = clon;
   const float L6 = -clon * clat, L7 = -slon * clat, L8 = -slat;
   quat_T(L.q, d.Ti2b);
-  const float c = (float)ce, s = (float)se;
-  // Tec2b = Ti2b * Tec2i, Tec2i = [c -s 0; s c 0; 0 0 1]
+  // Tl2b = Ti2b * Ti2l^T
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const float a = d.Ti2b[3 * i], b = d.Ti2b[3 * i + 1];
-    d.Tec2b[3 * i] = a * c + b * s;
-    d.Tec2b[3 * i + 1] = -a * s + b * c;
-    d.Tec2b[3 * i + 2] = d.Ti2b[3 * i + 2];
-  }
-  // Tl2b = Tec2b * Tl2ec (Tl2ec = Tec2l^T)
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float a = d.Tec2b[3 * i], b = d.Tec2b[3 * i + 1], e = d.Tec2b[3 * i + 2];
+    const float a = d.Ti2b[3 * i], b = d.Ti2b[3 * i + 1], e = d.Ti2b[3 * i + 2];
     d.Tl2b[3 * i] = a * L0 + b * L1 + e * L2;
     d.Tl2b[3 * i + 1] = a * L3 + b * L4;
     d.Tl2b[3 * i + 2] = a * L6 + b * L7 + e * L8;
@@ -635,9 +716,9 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
   const float gm = (float)GM_E * inv_r * inv_r;
   const float xy = 1.0f - 5.0f * slat * slat, zz = 3.0f - 5.0f * slat * slat;
   const float kxy = -gm * (1.0f + pre * xy);
-  d.gE[0] = kxy * clat * clon;
-  d.gE[1] = kxy * clat * slon;
-  d.gE[2] = -gm * (1.0f + pre * zz) * slat;
+  d.gI[0] = kxy * clat * clon;
+  d.gI[1] = kxy * clat * slon;
+  d.gI[2] = -gm * (1.0f + pre * zz) * slat;
 }
 
 __device__ __forceinline__ AltRef alt_ref(const Lane& L, double ce, double se) {
@@ -1040,12 +1121,13 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const float vg = d.vg;
   // pilot-station load factors from the PREVIOUS frame's accelerations (FGAuxiliary runs
   // before FGAccelerations)
-  float t1[3], t2[3], t3[3];
-  crossf(L.wId, C.eye, t1);
-  crossf(L.wI, C.eye, t2);
-  crossf(L.wI, t2, t3);
-  const float npy = (L.ba[1] + t1[1] + t3[1]) * C.inv_gref;
-  const float npz = (L.ba[2] + t1[2] + t3[2]) * C.inv_gref;
+  // (eye x w = -(w x eye): u1 = -(wId x eye), u3 = -(wI x (wI x eye)))
+  float u1[3], u2[3], u3[3];
+  cross_c(MP.eye, L.wId, u1);
+  cross_c(MP.eye, L.wI, u2);
+  crossf(L.wI, u2, u3);
+  const float npy = (L.ba[1] - u1[1] - u3[1]) * C.inv_gref;
+  const float npz = (L.ba[2] - u1[2] - u3[2]) * C.inv_gref;
   // -- Atmosphere (standard day: density altitude == altitude) --
   const float h = (float)d.h_ft;
   const Atm atm = atmosphere(h);
@@ -1053,7 +1135,8 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const float qbar = 0.5f * atm.rho * vt * vt;
   const float mach = vt * rcpf(atm.a);
   // h_b-mac = (h - (Tb2l * rp)_down) / b
-  const float vmac_d = d.Tl2b[2] * C.rp[0] + d.Tl2b[5] * C.rp[1] + d.Tl2b[8] * C.rp[2];
+  const float down_b[3] = {d.Tl2b[2], d.Tl2b[5], d.Tl2b[8]};
+  const float vmac_d = dot3c(MP.rp, down_b);
   const float hbmac = (h - vmac_d) * (1.0f / B_W);
   F16_STAMP(stamps, ST_ATM);
   // -- Systems (reads the previous frame's latch) --
@@ -1079,28 +1162,29 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F[1] = sb_ * fw0 + cb_ * fw1;
   F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
   float rxF[3];
-  crossf(C.rp, F, rxF);
+  cross_c(MP.rp, F, rxF);
   M[0] = A6[3] + rxF[0];
   M[1] = A6[4] + rxF[1];
   M[2] = A6[5] + rxF[2];
   // thrust along +x at the thruster: r x (T,0,0) = (0, rz T, -ry T)
   F[0] += thrust;
-  M[1] += C.eng[2] * thrust;
-  M[2] += -C.eng[1] * thrust;
+  if (MP.eng[2] != 0.0f) M[1] += MP.eng[2] * thrust;
+  if (MP.eng[1] != 0.0f) M[2] -= MP.eng[1] * thrust;
   F16_STAMP(stamps, ST_AERO);
   // -- Accelerations --
 #pragma unroll
-  for (int j = 0; j < 3; ++j) L.ba[j] = F[j] * C.inv_mass;
-  float gb[3];
-  mvec(d.Tec2b, d.gE, gb);
-  const float acc[3] = {L.ba[0] + gb[0], L.ba[1] + gb[1], L.ba[2] + gb[2]};
-  mtvec(d.Ti2b, acc, L.aI);
+  for (int j = 0; j < 3; ++j) L.ba[j] = F[j] * MP.inv_mass;
+  // inertial acceleration = Ti2b^T (specific force + body gravity) = Ti2b^T ba + gI
+  float abI[3];
+  mtvec(d.Ti2b, L.ba, abI);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) L.aI[j] = abI[j] + d.gI[j];
   float Jw[3], wxJw[3], rhs[3];
-  mvec(C.J, L.wI, Jw);
+  mvec_c(MP.J, L.wI, Jw);
   crossf(L.wI, Jw, wxJw);
 #pragma unroll
   for (int j = 0; j < 3; ++j) rhs[j] = M[j] - wxJw[j];
-  mvec(C.Jinv, rhs, L.wId);
+  mvec_c(MP.Jinv, rhs, L.wId);
   // -- Auxiliary latch for the next frame's FCS --
   if (LOWREG) __builtin_amdgcn_sched_barrier(0);
   L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;

@@ -1179,7 +1179,7 @@ __device__ void trim_residual(const double* icb, const float* x, const float* T,
   Derived d;
   derive(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), d);
   float gb[3];
-  mvec(d.Tec2b, d.gE, gb);
+  mvec(d.Ti2b, d.gI, gb);
   const float we = (float)OMEGA_E;
   const float wb[3] = {d.Ti2b[2] * we, d.Ti2b[5] * we, d.Ti2b[8] * we};
   const float t[3] = {d.pqr[0] + 2.0f * wb[0], d.pqr[1] + 2.0f * wb[1], d.pqr[2] + 2.0f * wb[2]};
@@ -1390,47 +1390,9 @@ static void soa_carve(void* base, int64_t n, SoA& s) {
 }
 static size_t soa_bytes(int64_t n) { return (size_t)n * NCOL_ALL * 16; }
 
-// Same mass-balance / constants derivation as oracle init_consts() (f16.xml:37-83,245-300).
+// Same constants derivation as oracle init_consts() (f16.xml:37-83,245-300); the mass
+// properties are compile-time constants (f16_device.h f16_mass_props, shared with the kernels).
 static void build_consts(const f16env_config& cfg, ModelConsts& C) {
-  const double SLUG2LB = 32.174049, IN2FT = 1.0 / 12.0;
-  const double empty = 17400.0, cg_e[3] = {-193.0, 0.0, -5.1};
-  const double pilot = 230.0, pilot_loc[3] = {-336.2, 0.0, 0.0};
-  const double tank_w[4] = {1000.0, 1000.0, 0.0, 0.0};
-  const double tank_loc[4][3] = {{-174.4, 65.0, 5.0}, {-174.4, -65.0, 5.0}, {-174.4, 65.0, -15.0}, {-174.4, -65.0, -15.0}};
-  double W = empty + pilot, m[3], cg[3];
-  for (int i = 0; i < 3; ++i) m[i] = empty * cg_e[i] + pilot * pilot_loc[i];
-  for (int t = 0; t < 4; ++t) {
-    W += tank_w[t];
-    for (int i = 0; i < 3; ++i) m[i] += tank_w[t] * tank_loc[t][i];
-  }
-  for (int i = 0; i < 3; ++i) cg[i] = m[i] / W;
-  const double mass = W / SLUG2LB;
-  double J[9] = {9496, 0, -982, 0, 55814, 0, -982, 0, 63100};
-  auto s2b = [&](const double* r, double* o) {
-    o[0] = IN2FT * (cg[0] - r[0]); o[1] = IN2FT * (r[1] - cg[1]); o[2] = IN2FT * (cg[2] - r[2]);
-  };
-  auto pm = [&](double mm, const double* v) {
-    const double sv[3] = {mm * v[0], mm * v[1], mm * v[2]};
-    const double xx = sv[0] * v[0], yy = sv[1] * v[1], zz = sv[2] * v[2];
-    const double xy = -sv[0] * v[1], xz = -sv[0] * v[2], yz = -sv[1] * v[2];
-    J[0] += yy + zz; J[1] += xy; J[2] += xz; J[3] += xy; J[4] += xx + zz; J[5] += yz;
-    J[6] += xz; J[7] += yz; J[8] += xx + yy;
-  };
-  double v[3];
-  s2b(pilot_loc, v);
-  pm(pilot / SLUG2LB, v);
-  for (int t = 0; t < 4; ++t) { s2b(tank_loc[t], v); pm(tank_w[t] / SLUG2LB, v); }
-  const double a = J[0], b = J[1], c = J[2], d = J[3], e = J[4], f = J[5], g = J[6], h = J[7], k = J[8];
-  const double A = e * k - f * h, B = -(d * k - f * g), Cc = d * h - e * g;
-  const double det = a * A + b * B + c * Cc, r = 1.0 / det;
-  const double Ji[9] = {A * r, -(b * k - c * h) * r, (b * f - c * e) * r, B * r, (a * k - c * g) * r,
-                        -(a * f - c * d) * r, Cc * r, -(a * h - b * g) * r, (a * e - b * d) * r};
-  C.inv_mass = (float)(1.0 / mass);
-  for (int i = 0; i < 9; ++i) { C.J[i] = (float)J[i]; C.Jinv[i] = (float)Ji[i]; }
-  const double aerorp[3] = {-189.5, 0.0, 3.9}, eye[3] = {-336.2, 0.0, 29.5}, eng[3] = {0, 0, 0};
-  s2b(aerorp, v); for (int i = 0; i < 3; ++i) C.rp[i] = (float)v[i];
-  s2b(eye, v); for (int i = 0; i < 3; ++i) C.eye[i] = (float)v[i];
-  s2b(eng, v); for (int i = 0; i < 3; ++i) C.eng[i] = (float)v[i];
   C.inv_gref = (float)((WGS_A * WGS_A) / GM_E);
   // US-76 sea level in JSBSim units
   const double R = 8.31432 / 0.0289644;
