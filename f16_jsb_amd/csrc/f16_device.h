@@ -286,7 +286,9 @@ __device__ __forceinline__ void lane_load_lds(const float4* cols, Lane& L) {
   lane_unpack<false>(c, z, z, L);
 }
 
-template <bool GUST = false>
+// PART: 0 every column; 1 the columns a step's frames leave final (all but C3 and C15, which
+// the env layer still changes: episode return, last distance, and a reset); 2 C3 and C15.
+template <bool GUST = false, int PART = 0>
 __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
   const int64_t n = s.n;
   float4 c[NCOL];
@@ -309,8 +311,9 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
                       __int_as_float(L.step), __int_as_float(L.ep_count));
   float4* p = s.c + k;
 #pragma unroll
-  for (int j = 0; j < NCOL; ++j, p += n) *p = c[j];
-  if (GUST) {
+  for (int j = 0; j < NCOL; ++j, p += n)
+    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) *p = c[j];
+  if (GUST && PART != 2) {
     *p = make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f);
     *(p + n) = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
   }

@@ -589,6 +589,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
   float rew_out = 0.0f;
   int flags_out = 0;
+  double ce = 1.0, se = 0.0;
+  AltRef A;
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
@@ -601,10 +603,22 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         L.wind[j] = L.wst[j] + L.gust[j];
       }
     }
-    double ce, se;
     earth_angle(L.epa, ce, se);
-    const AltRef A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
+    A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
     for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+  }
+  // Two-waves-per-SIMD builds with no done list to compact (its atomic's return would wait
+  // for every store before it): retire the stack DMA and store the state columns the frames
+  // left final now, so their drain overlaps the observation frame, reward and stack rebuild
+  // (and the partner wave's work) instead of adding to the tail. Measured (gpurun r02m, MODE 0):
+  // 131 072 envs 30.35 -> 29.89 us, 262 144 62.35 -> 60.0 us; at one wave per SIMD it gained
+  // nothing at 65 536 envs and cost 0.4 us at 4 096, so the one-wave build keeps one store tail.
+  const bool early_store = LOWREG && !a.done_idx;
+  if (early_store) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (live) lane_store<GUST, 1>(a.s, k, L);
+  }
+  if (live) {
     make_frame(L, ce, se, A, f);                              // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261), PositionReward (:493-507)
@@ -616,7 +630,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   }
   // the stack DMA issued after the prologue has long landed; retire it here, before any
   // store of this step (vmcnt also counts stores on CDNA, so a later wait would drain them)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // -- unless the early state store above already did
+  if (!early_store) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // compaction of finished lanes (wave64 ballot), before any store of this step so the
   // atomic's return waits on nothing else
   if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)
@@ -653,7 +668,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     }
     F16_STAMP(stamps, ST_RESET);
 #ifndef F16_DIAG_SKIP_STORE
-    lane_store<GUST>(a.s, k, L);
+    if (!early_store || (done && !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
+      lane_store<GUST>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
+    else
+      lane_store<GUST, 2>(a.s, k, L);  // the rest
 #else
     if (L.step == -12345) lane_store<GUST>(a.s, k, L);
 #endif
