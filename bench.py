@@ -7,11 +7,14 @@
 A "step" is one VecEnv step (4 FDM frames + obs/reward/termination/auto-reset) of every env
 on the GPU, driven through the device-tensor VecEnv boundary (F16Envs.step) with random
 actions from the device Philox stream, pre-generated into HBM before the timed region.
+The observation layout is the windowed one (F16Envs(obs_layout="window"): the (N, K, 15)
+obs is a strided view of per-env frame histories, one new 64-B frame slot written per step);
+the contiguous ping-pong layout is timed beside it (`layouts`).
 Envs shard across ranks (weak scaling, no collective in the stepping loop); the job-level
 value is all ranks' env-steps divided by the max-over-ranks wall time.
 
 Prints ONE JSON line on rank 0 (driver contract), including
-  roofline     -- algorithmic HBM bytes per launch of f16_step_kernel / its average launch
+  roofline     -- algorithmic HBM bytes per launch of the step kernel / its average launch
                   duration (HIP events on the launch stream), vs the 8 TB/s HBM peak;
                   `traffic` = PMC-measured HBM bytes per launch from profiles/ if present;
   cpu_baseline -- the CPU oracle (oracle/f16ref.c, fp64 C restatement, OpenMP) timed on this
@@ -45,6 +48,8 @@ def parse():
                     help="cfg3: the headline (reference task); cfg5: random ICs + wind gusts")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (cfg3 65536, cfg5 131072)")
     ap.add_argument("--stack", type=int, default=4)
+    ap.add_argument("--obs-layout", choices=("window", "contiguous"), default="window",
+                    help="observation layout of the headline (the other is timed beside it at N=1)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -248,20 +253,30 @@ def features_bench(envs, stream, iters=200):
     gbps = frames * (15 + 17) * 4 / (ms * 1e-3) / 1e9
     # the same features emitted alongside obs by the step call (F16Envs.step(..., features=)):
     # marginal cost per step vs a plain step, same actions
+    # (the window layout has no fused form: the step, then f16env_features_strided on the view)
     n = obs.shape[0]
     act = envs.sample_actions(99, 0)
+
+    def stepf(use):
+        if envs.window:
+            o = envs.step(act).obs
+            if use:
+                features(o, out)
+        else:
+            envs.step(act, features=out if use else None)
+
     for _ in range(5):
-        envs.step(act, features=out)
+        stepf(True)
     t = []
     for use in (False, True, False, True):
         s.record(stream)
         for _ in range(iters // 2):
-            envs.step(act, features=out if use else None)
+            stepf(use)
         e.record(stream)
         torch.cuda.synchronize()
         t.append(s.elapsed_time(e) / (iters // 2))
     plain, fused = min(t[0], t[2]), min(t[1], t[3])
-    return {"kernel": "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
+    return {"kernel": "f16_features_strided_kernel" if envs.window else "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
             "frames_per_s": round(frames / (ms * 1e-3), 1), "achieved_GBps": round(gbps, 1),
             "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128,
             "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5)}
@@ -388,21 +403,51 @@ def sb3_compat_bench(dev, n, steps=20):
                     "PCIe-inclusive: pinned staging, one obs + one packed flag copy, shared info for running lanes)"}
 
 
-def load_traffic(envs, stack, state_bytes):
-    """Per-launch HBM bytes of f16_step_kernel from the committed PMC summary, if it was
-    measured on this workload and state layout."""
+def layout_leg(dev, args, layout, steps=300):
+    """The headline workload in the other observation layout, beside the headline (N=1): same
+    phase spread + burn-in, `steps` timed steps (region HIP events) and the kernel's own
+    per-launch duration (dispatch events)."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    e = F16Envs(args.envs, stack_k=args.stack, device=dev, seed=args.seed, obs_layout=layout)
+    e.reset()
+    spread_phases(e, args, dev)
+    acts = [e.sample_actions(args.seed + 1000, t) for t in range(16)]
+    stream = torch.cuda.current_stream(dev)
+    s, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record(stream)
+    for t in range(steps):
+        e.step(acts[t % 16])
+    en.record(stream)
+    torch.cuda.synchronize()
+    region = s.elapsed_time(en) / steps
+    kern_ms, _, _ = e.profile_kernel(lambda: [e.step(acts[t % 16]) for t in range(steps)], steps)
+    b = e.algorithmic_bytes_per_env_step()
+    out = {"layout": layout, "kernel": e.step_kernel_name, "region_ms_per_step": round(region, 5),
+           "kernel_ms": round(kern_ms, 5), "env_steps_per_s_region": round(args.envs / (region * 1e-3), 1),
+           "algorithmic_bytes_per_env_step": b,
+           "frac_of_hbm_peak": round(b * args.envs / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+    e.close()
+    return out
+
+
+def load_traffic(envs, stack, state_bytes, layout):
+    """Per-launch HBM bytes of the step kernel from the committed PMC summary, if it was
+    measured on this workload, state size and observation layout."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("envs") == envs and d.get("stack_k") == stack and d.get("state_bytes") == state_bytes:
+        if (d.get("envs") == envs and d.get("stack_k") == stack and d.get("state_bytes") == state_bytes
+                and d.get("layout", "contiguous") == layout):
             return d.get("hbm_bytes_per_launch")
     except Exception:  # noqa: BLE001
         pass
     return None
 
 
-def load_valu(envs, stack):
+def load_valu(envs, stack, kernel):
     """VALU side of the step kernel (SURVEY 8(d) asks for it beside the HBM fraction): the
     committed SQ-counter summary (tools/pmc_valu.py), if it was measured on this workload.
     The VALU issue peak for one wave per SIMD is one wave64 instruction per 4 cycles."""
@@ -410,7 +455,7 @@ def load_valu(envs, stack):
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("envs") == envs and d.get("stack_k") == stack:
+        if d.get("envs") == envs and d.get("stack_k") == stack and d.get("kernel") == kernel.split("<")[0]:
             return {"valu_insts_per_wave_step": d["valu_insts_per_wave_step"], "valu_busy_frac": d["valu_busy_frac"],
                     "wait_any_frac": d["wait_any_frac"], "wave_cycles": d["wave_cycles"],
                     "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_* passes)"}
@@ -446,7 +491,7 @@ def main():
         args.envs = 131072 if cfg5 else 65536
     n = args.envs
     venv = F16VecEnv(num_envs=n, stack_k=args.stack, device=dev, seed=args.seed, return_numpy=False,
-                     env_id_base=rank * n, cfg5=cfg5)
+                     env_id_base=rank * n, cfg5=cfg5, obs_layout=args.obs_layout)
     envs = venv.envs
     kernel_name, waves_per_simd = envs.step_kernel_name, envs.waves_per_simd
     venv.reset()
@@ -505,6 +550,8 @@ def main():
     sb3 = sb3_compat_bench(dev, n) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
     cfg2 = cfg2_bench(dev) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
     persist = persistent_bench(dev, n, args.stack, 1000, args.seed + 6000) if (world == 1 and not cfg5) else None
+    other = "contiguous" if args.obs_layout == "window" else "window"
+    layouts = layout_leg(dev, args, other) if (world == 1 and not cfg5) else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
         rollout = rollout_bench(args, dev, rank, world)
@@ -515,6 +562,7 @@ def main():
     total_env_steps = n * world * args.steps
     value = total_env_steps / elapsed
     bytes_per_env_step = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
+    stack_bytes = envs.stack_bytes_per_env_step() + (24 if cfg5 else 0)
     bytes_per_launch = bytes_per_env_step * n
     # launch duration used for the roofline: the kernel's average execution time from its own
     # dispatch events (what rocprofv3 --kernel-trace reports); the timed region's GPU time per
@@ -522,7 +570,7 @@ def main():
     # (cfg5: the step is two kernels -- step + deferred reset -- so the region time is used)
     roof_ms = gpu_ms_per_step if cfg5 else kern_ms
     achieved = bytes_per_launch / (roof_ms * 1e-3) / 1e9
-    traffic = None if cfg5 else load_traffic(n, args.stack, envs.state_bytes_per_env)
+    traffic = None if cfg5 else load_traffic(n, args.stack, envs.state_bytes_per_env, args.obs_layout)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -559,7 +607,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
-            "valu": None if cfg5 else load_valu(n, args.stack),
+            "valu": None if cfg5 else load_valu(n, args.stack, kernel_name),
             "kernel": kernel_name + (" + f16_reset_done_kernel" if cfg5 else ""),
             "waves_per_simd": waves_per_simd,
             "kernel_ms": round(roof_ms, 5),
@@ -570,6 +618,13 @@ def main():
             "region_ms_per_launch": round(gpu_ms_per_step, 5),
             "region_timing": "HIP events around the timed region on the launch stream / launches",
             "algorithmic_bytes_per_env_step": bytes_per_env_step,
+            "bytes_basis": ("windowed obs: 16 + 2*60 + 4 + 2 + 2S (new frame to both histories; frame "
+                            "slots are 64 B)" if args.obs_layout == "window" else "SURVEY 8(d) B(K)"),
+            # SURVEY 8(d)'s B(K) -- the bytes of the same step with the stack materialised --
+            # over the same launch time: the rate the contiguous layout would need to match it
+            "stack_equivalent_bytes_per_env_step": stack_bytes,
+            "stack_equivalent_frac": round(stack_bytes * n / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "obs_layout": args.obs_layout,
             "launch_env_steps": n,
         },
         "episode_mix": {
@@ -589,6 +644,10 @@ def main():
         out["cfg2"] = cfg2
     if persist is not None:
         out["persistent_random_policy"] = persist
+    if layouts is not None:
+        out["layouts"] = {args.obs_layout: {"kernel": kernel_name, "kernel_ms": round(kern_ms, 5),
+                                            "region_ms_per_step": round(gpu_ms_per_step, 5)},
+                          other: layouts}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
     print(json.dumps(out), flush=True)

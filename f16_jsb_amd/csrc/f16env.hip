@@ -482,39 +482,27 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
 // frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
 // 160 KB). sT is then unused.
-// Windowed observations (WIN, f16env_step_window): per env two frame histories [T][15] (wx:
-// this step's parity, wy: the other), the observation of a step being the view
-// wx[k][p-K+1 .. p] (strides T*15, 15, 1). A step writes its new frame at position p of BOTH
-// histories -- no stack shift copy, no previous-stack read -- with 16-B stores at the
-// position's uniform phase (put_frame). Lanes reset right before this step (FRESH) fill
-// wx[p-K+1 .. p-1] with their reset frame (LDS-DMA'd from wy[p-1], which that reset wrote);
-// lanes reset by this step fill wx[p-K+1 .. p] with the new reset frame and keep their final
-// frame in wy[p], so wy's window IS the terminal observation (no copy). The other parity's
-// window is untouched by a step, so an observation stays valid until the step after next, as
-// with the ping-pong buffers of f16env_step.
-// One frame (15 floats) to a history row at float phase pf = (frame start mod 4), uniform per
-// launch: whole 16-B stores between a 1-3 float head and tail (4 or 5 store instructions).
-typedef float f2s __attribute__((ext_vector_type(2)));
-typedef float f3s __attribute__((ext_vector_type(3)));
-__device__ __forceinline__ void put_frame(float* d, const float* f, int pf) {
-  auto q4 = [&](int o, int j) { *reinterpret_cast<float4*>(d + o) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]); };
-  if (pf == 0) {
-    q4(0, 0); q4(4, 4); q4(8, 8);
-    *reinterpret_cast<f3s*>(d + 12) = f3s{f[12], f[13], f[14]};
-  } else if (pf == 1) {
-    *reinterpret_cast<f3s*>(d) = f3s{f[0], f[1], f[2]};
-    q4(3, 3); q4(7, 7); q4(11, 11);
-  } else if (pf == 2) {
-    *reinterpret_cast<f2s*>(d) = f2s{f[0], f[1]};
-    q4(2, 2); q4(6, 6); q4(10, 10);
-    d[14] = f[14];
-  } else {
-    d[0] = f[0];
-    q4(1, 1); q4(5, 5); q4(9, 9);
-    *reinterpret_cast<f2s*>(d + 13) = f2s{f[13], f[14]};
-  }
+// Windowed observations (WIN, f16env_step_window): per env two frame histories [T][16] (wx:
+// this step's parity, wy: the other; 16-float = 64-B frame slots, the 16th float 0), the
+// observation of a step being the view wx[k][p-K+1 .. p][0..15) (strides T*16, 16, 1). A step
+// writes its new frame at position p of BOTH histories -- no stack shift copy, no
+// previous-stack read -- as four aligned 16-B stores filling one whole 64-B sector (a 60-B
+// frame at a 60-B pitch leaves partial sectors, which cost as much as the whole-row rewrite
+// they replace: 22.6 vs 18.5 us per step at 65 536 envs, K = 4, gpurun r02n). Lanes reset right
+// before this step (FRESH) fill wx[p-K+1 .. p-1] with their reset frame (LDS-DMA'd from
+// wy[p-1], which that reset wrote); lanes reset by this step fill wx[p-K+1 .. p] with the new
+// reset frame and keep their final frame in wy[p], so wy's window IS the terminal observation
+// (no copy). The other parity's window is untouched by a step, so an observation stays valid
+// until the step after next, as with the ping-pong buffers of f16env_step.
+static constexpr int WPITCH = 16;  // floats per history frame slot
+__device__ __forceinline__ void put_slot(float* d, const float* f) {
+  float4* q = reinterpret_cast<float4*>(d);
+  q[0] = make_float4(f[0], f[1], f[2], f[3]);
+  q[1] = make_float4(f[4], f[5], f[6], f[7]);
+  q[2] = make_float4(f[8], f[9], f[10], f[11]);
+  q[3] = make_float4(f[12], f[13], f[14], 0.0f);
 }
-static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([15][64])
+static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([4][64] float4)
 
 template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
@@ -581,9 +569,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     L.flags &= ~LANE_FLAG_FRESH;
   }
   if (WIN && fresh && a.E.K > 1) {
-    const float* src = a.wy + k * a.wrow + (int64_t)(a.wpos - 1) * F16_OBS_DIM;
+    const float* src = a.wy + k * a.wrow + (int64_t)(a.wpos - 1) * WPITCH;
 #pragma unroll
-    for (int j = 0; j < F16_OBS_DIM; ++j) dma4(src + j, stg + j * 64);
+    for (int j = 0; j < 4; ++j) dma16(src + 4 * j, stg + j * 256);  // [j][lane] float4
   }
   F16_STAMP(stamps, ST_LOAD);
   float f[F16_OBS_DIM], f0[F16_OBS_DIM];
@@ -719,21 +707,23 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     if (live && K > 1 && (fresh || reset_now)) {  // rare: whole-window fills of reset lanes
       float* X = a.wx + k * a.wrow;
       if (fresh) {
-        float f0p[F16_OBS_DIM];
+        float f0p[16];
 #pragma unroll
-        for (int j = 0; j < F16_OBS_DIM; ++j) f0p[j] = stg[j * 64 + lane];
-        for (int r = p - K + 1; r < p; ++r) put_frame(X + (int64_t)r * F16_OBS_DIM, f0p, (4 - (r & 3)) & 3);
+        for (int j = 0; j < 4; ++j) {
+          const float4 v = reinterpret_cast<const float4*>(stg)[j * 64 + lane];
+          f0p[4 * j] = v.x; f0p[4 * j + 1] = v.y; f0p[4 * j + 2] = v.z; f0p[4 * j + 3] = v.w;
+        }
+        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * WPITCH, f0p);
       }
       if (reset_now)  // after the fresh fill: a one-step episode ends in its own reset window
-        for (int r = p - K + 1; r < p; ++r) put_frame(X + (int64_t)r * F16_OBS_DIM, f0, (4 - (r & 3)) & 3);
+        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * WPITCH, f0);
     }
     // this step's frame at position p of both histories (wx: the reset frame of a lane reset
     // now, else the new frame; wy: the new frame), aligned stores at the uniform phase
     if (live) {
-      const int pf = (4 - (p & 3)) & 3;
-      const int64_t off = k * a.wrow + (int64_t)p * F16_OBS_DIM;
-      put_frame(a.wx + off, reset_now ? f0 : f, pf);
-      put_frame(a.wy + off, f, pf);
+      const int64_t off = k * a.wrow + (int64_t)p * WPITCH;
+      put_slot(a.wx + off, reset_now ? f0 : f);
+      put_slot(a.wy + off, f);
     }
     F16_STAMP(stamps, ST_COPY);
   } else if (kSkipStack) {
@@ -1024,8 +1014,10 @@ struct ResetDoneArgs {
   SoA s, tmpl;
   const int32_t* done_idx;
   const int32_t* n_done;
-  float* obs;       // row of env k: obs + k * obs_row + obs_off (contiguous: K*15, 0; window: T*15, (p-K+1)*15)
+  float* obs;       // row of env k: obs + k * obs_row + obs_off, frames obs_pitch floats apart
+                    // (contiguous: K*15, 0, 15; window: T*16, (p-K+1)*16, 16)
   int64_t obs_row, obs_off;
+  int32_t obs_pitch;
   EnvArgs E;
   ModelConsts C;
 };
@@ -1044,7 +1036,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
     lane_store<true>(a.s, k, L);
     float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
-      for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
+      for (int j = 0; j < a.obs_pitch; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
   }
 }
 
@@ -1055,6 +1047,7 @@ struct ResetArgs {
   const double* ic;
   float* obs;       // row addressing as ResetDoneArgs
   int64_t obs_row, obs_off;
+  int32_t obs_pitch;
   int* wind_any;    // per-lane IC given: set if a lane got wind (the handle needs the wind kernels)
   EnvArgs E;
   ModelConsts C;
@@ -1078,20 +1071,20 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   if (a.obs) {
     float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
-      for (int j = 0; j < F16_OBS_DIM; ++j) o[r * F16_OBS_DIM + j] = f0[j];
+      for (int j = 0; j < a.obs_pitch; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
   }
 }
 
 // windowed observations: the histories' last K-1 frames (positions p_old-K+2 .. p_old) move
 // to the front (0 .. K-2) of both histories, so the next step writes its frame at K-1
 __global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wrow, int32_t p_old, float* h0, float* h1) {
-  const int64_t per = (int64_t)(K - 1) * F16_OBS_DIM;
+  const int64_t per = (int64_t)(K - 1) * WPITCH;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * n * per) return;
   const int64_t b = i / (n * per), r = i - b * n * per;
   const int64_t k = r / per, j = r - k * per;
   float* row = (b ? h1 : h0) + k * wrow;
-  row[j] = row[(int64_t)(p_old - K + 2) * F16_OBS_DIM + j];
+  row[j] = row[(int64_t)(p_old - K + 2) * WPITCH + j];
 }
 
 // IC -> state (used once at create to build the reset template, n = 1)
@@ -1332,6 +1325,48 @@ __global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, con
   if (t < nf) frame_features(sIn + t * FEAT_IN, sOut + t * FEAT_OUT);
   __syncthreads();
   if (vout) {
+    for (int q = t; q < 256 * FEAT_OUT / 4; q += 256)
+      reinterpret_cast<float4*>(gout)[q] = reinterpret_cast<const float4*>(sOut)[q];
+  } else {
+    for (int q = t; q < nf * FEAT_OUT; q += 256) gout[q] = sOut[q];
+  }
+}
+
+// The same per-frame transform on a strided (B, K, 15) block -- e.g. a windowed observation
+// (rows T*16 floats apart, 64-B frame slots) read in place, no copy to a contiguous stack.
+// One lane per frame (16-B vector reads of its slot when the strides allow); the (B, K, 17)
+// output leaves through LDS as coalesced float4, as in f16_features_kernel.
+__global__ __launch_bounds__(256) void f16_features_strided_kernel(int64_t n_rows, int32_t K, const float* __restrict__ obs,
+                                                                   int64_t row_stride, int64_t frame_stride,
+                                                                   float* __restrict__ feat) {
+  __shared__ __align__(16) float sOut[256 * FEAT_OUT];
+  const int64_t n_frames = n_rows * K;
+  const int64_t f0 = (int64_t)blockIdx.x * 256;
+  const int nf = (int)(n_frames - f0 < 256 ? n_frames - f0 : 256);
+  const int t = threadIdx.x;
+  if (t < nf) {
+    const int64_t i = f0 + t;
+    const int64_t r = i / K, kk = i - r * K;
+    const float* o = obs + r * row_stride + kk * frame_stride;
+    float x[FEAT_IN];
+    if ((frame_stride & 3) == 0 && (row_stride & 3) == 0 && ((uintptr_t)obs & 15) == 0) {  // 16-B aligned frames
+      const float4* q = reinterpret_cast<const float4*>(o);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 v = q[j];
+        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+      }
+      const float2 v2 = *reinterpret_cast<const float2*>(o + 12);
+      x[12] = v2.x; x[13] = v2.y; x[14] = o[14];
+    } else {
+#pragma unroll
+      for (int j = 0; j < FEAT_IN; ++j) x[j] = o[j];
+    }
+    frame_features(x, sOut + t * FEAT_OUT);
+  }
+  __syncthreads();
+  float* gout = feat + f0 * FEAT_OUT;
+  if (nf == 256 && (((uintptr_t)gout) & 15) == 0) {
     for (int q = t; q < 256 * FEAT_OUT / 4; q += 256)
       reinterpret_cast<float4*>(gout)[q] = reinterpret_cast<const float4*>(sOut)[q];
   } else {
@@ -1663,7 +1698,7 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   if (!h) return set_err(-1, "null handle");
   ResetArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = obs;
-  a.obs_row = (int64_t)h->cfg.stack_k * F16_OBS_DIM; a.obs_off = 0;
+  a.obs_row = (int64_t)h->cfg.stack_k * F16_OBS_DIM; a.obs_off = 0; a.obs_pitch = F16_OBS_DIM;
   a.E = env_args(h);
   a.C = h->C;
   return reset_launch(h, (hipStream_t)stream, a);
@@ -1715,7 +1750,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = obs;
-    r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0;
+    r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0; r.obs_pitch = F16_OBS_DIM;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1742,7 +1777,7 @@ static int window_check(f16env_t h, const float* hist_cur, const float* hist_oth
   if (!hist_cur || (hist_other == nullptr && hist_cur == nullptr)) return set_err(-1, "null history");
   if (((uintptr_t)hist_cur & 15) != 0 || ((uintptr_t)hist_other & 15) != 0)
     return set_err(-1, "histories must be 16-byte aligned");
-  if (T % 4 != 0 || T < 2 * (int64_t)K) return set_err(-1, "history length T must be a multiple of 4 and >= 2K");
+  if (T < 2 * (int64_t)K) return set_err(-1, "history length T must be >= 2K");
   if (pos < K - 1 || (int64_t)pos >= T) return set_err(-1, "window position must be in [K-1, T-1]");
   return 0;
 }
@@ -1763,7 +1798,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   a.term = terminated; a.trunc = truncated; a.ep_ret = ep_return; a.ep_len = ep_len;
   a.done_idx = done_idx; a.n_done = n_done;
   a.nonfinite = h->nonfinite;
-  a.wx = hist_cur; a.wy = hist_other; a.wrow = T * F16_OBS_DIM; a.wpos = pos;
+  a.wx = hist_cur; a.wy = hist_other; a.wrow = T * WPITCH; a.wpos = pos;
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = 0;
@@ -1785,7 +1820,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
-    r.obs_row = T * F16_OBS_DIM; r.obs_off = (int64_t)(pos - a.E.K + 1) * F16_OBS_DIM;
+    r.obs_row = T * WPITCH; r.obs_off = (int64_t)(pos - a.E.K + 1) * WPITCH; r.obs_pitch = WPITCH;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1800,7 +1835,7 @@ int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const flo
   if (int e = window_check(h, hist_cur, nullptr, T, pos)) return e;
   ResetArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = hist_cur;
-  a.obs_row = T * F16_OBS_DIM; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * F16_OBS_DIM;
+  a.obs_row = T * WPITCH; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * WPITCH; a.obs_pitch = WPITCH;
   a.E = env_args(h);
   a.C = h->C;
   return reset_launch(h, (hipStream_t)stream, a);
@@ -1813,9 +1848,9 @@ int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, 
   const int K = h->cfg.stack_k;
   if (K < 2) return 0;
   if (pos_old - K + 2 <= K - 2) return set_err(-1, "restart source and destination overlap (pos_old < 2K-3)");
-  const int64_t total = 2 * (int64_t)h->cfg.n_envs * (K - 1) * F16_OBS_DIM;
+  const int64_t total = 2 * (int64_t)h->cfg.n_envs * (K - 1) * WPITCH;
   hipLaunchKernelGGL(f16_window_restart_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, (int64_t)h->cfg.n_envs, (int32_t)K, T * F16_OBS_DIM, pos_old, hist0, hist1);
+                     (hipStream_t)stream, (int64_t)h->cfg.n_envs, (int32_t)K, T * WPITCH, pos_old, hist0, hist1);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1923,6 +1958,22 @@ int f16env_features(void* stream, int64_t n_frames, const float* obs, float* fea
   if (blocks > 0x7fffffffLL) return set_err(-1, "n_frames too large");
   hipLaunchKernelGGL(f16_features_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_frames, obs,
                      feat);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float* obs, int64_t row_stride,
+                            int64_t frame_stride, float* feat) {
+  if (n_rows < 0 || K < 1) return set_err(-1, "n_rows >= 0 and K >= 1 required");
+  if (n_rows == 0) return 0;
+  if (!obs || !feat) return set_err(-1, "null argument");
+  if (frame_stride < F16_OBS_DIM || row_stride < (int64_t)(K - 1) * frame_stride + F16_OBS_DIM)
+    return set_err(-1, "frames overlap (frame_stride >= 15, row_stride >= (K-1) frame_stride + 15)");
+  if (((uintptr_t)obs & 3) != 0 || ((uintptr_t)feat & 3) != 0) return set_err(-1, "obs and feat must be float-aligned");
+  const int64_t blocks = (n_rows * K + 255) / 256;
+  if (blocks > 0x7fffffffLL) return set_err(-1, "too many frames");
+  hipLaunchKernelGGL(f16_features_strided_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_rows, K,
+                     obs, row_stride, frame_stride, feat);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -45,6 +45,15 @@ def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+def _default_history(k: int) -> int:
+    """Default window history T: 124 slots (row stride 124 x 64 B = 4 x 31 slots), or the next
+    4 x odd >= 2K for long stacks."""
+    T = 124
+    while T < 2 * k:
+        T += 8
+    return T
+
+
 class F16Envs:
     """N F-16 envs on one GPU behind the C ABI. All tensors are torch tensors on ``device``."""
 
@@ -54,10 +63,13 @@ class F16Envs:
                  history: int = 0, **cfg_kw):
         """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
-        `history` frames (f16env_step_window: only the new frame is written per step; strides
-        (T*15, 15, 1), so obs.reshape(N, K*15) is still a view); history 0 = max(128, 4K)
-        rounded up to a multiple of 4. Both layouts give identical values and the same
-        validity (an observation stays valid until the step after next)."""
+        `history` 64-B frame slots (f16env_step_window: only the new frame is written per step;
+        strides (T*16, 16, 1)); history 0 = 124 or, for K > 62, the next 4 x odd >= 2K (a row
+        stride of 4 x odd 64-B slots spreads the rows over the HBM channels; 127-129 measured
+        slow, profiles/r02_layout_ab.json). Both
+        layouts give identical values and the same validity (an observation stays valid until
+        the step after next). A consumer that needs a flat (N, K*15) array copies the window
+        (reshape); the features kernel (f16_jsb_amd.features) reads it in place."""
         import torch
 
         if not torch.cuda.is_available():
@@ -84,12 +96,11 @@ class F16Envs:
             raise ValueError("obs_layout must be 'contiguous' or 'window'")
         self.window = obs_layout == "window"
         if self.window:
-            T = int(history) if history else max(128, 4 * k)
-            T = (T + 3) // 4 * 4
+            T = int(history) if history else _default_history(k)
             if T < 2 * k:
                 raise ValueError("history must be >= 2 * stack_k")
             self.T = T
-            self._hist = torch.zeros((2, n, T, F16_OBS_DIM), dtype=f32, device=dev)
+            self._hist = torch.zeros((2, n, T, 16), dtype=f32, device=dev)  # 64-B frame slots
             self._hist_ptr = (self._hist[0].data_ptr(), self._hist[1].data_ptr())
             self._p = k - 1   # newest frame position of the current observation's window
             self._obs = None
@@ -130,7 +141,7 @@ class F16Envs:
     def _window(self, other: int = 0):
         """(N, K, 15) view of the current (other=0) or other-parity history's window."""
         p = self._p
-        return self._hist[self._cur ^ other, :, p - self.k + 1:p + 1]
+        return self._hist[self._cur ^ other, :, p - self.k + 1:p + 1, :F16_OBS_DIM]
 
     def _no_window(self, what: str):
         if self.window:
@@ -174,6 +185,12 @@ class F16Envs:
         return int(lib().f16env_state_bytes_per_env())
 
     def algorithmic_bytes_per_env_step(self) -> int:
+        """Bytes per env step of this handle's layout (abi.algorithmic_bytes_per_env_step)."""
+        return algorithmic_bytes_per_env_step(self.k, self.state_bytes_per_env,
+                                              "window" if self.window else "contiguous")
+
+    def stack_bytes_per_env_step(self) -> int:
+        """SURVEY.md 8(d)'s B(K): the bytes of the same step with the stack materialised."""
         return algorithmic_bytes_per_env_step(self.k, self.state_bytes_per_env)
 
     # --------------------------------------------------------------------------------------
@@ -377,8 +394,8 @@ class F16Envs:
         o = self.torch.as_tensor(obs, dtype=self.torch.float32)
         if self.window:
             p, k = self._p, self.k
-            self._hist[0, :, p - k + 1:p + 1].copy_(o)
-            self._hist[1, :, p - k + 1:p + 1].copy_(o)
+            self._hist[0, :, p - k + 1:p + 1, :F16_OBS_DIM].copy_(o)
+            self._hist[1, :, p - k + 1:p + 1, :F16_OBS_DIM].copy_(o)
         else:
             self._obs[self._cur].copy_(o)
 

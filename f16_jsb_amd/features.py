@@ -30,6 +30,19 @@ def features(obs: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         raise ValueError("last dimension must be %d (jsbsim_gym.py:12-25 + goal), got %s" % (OBS_DIM, tuple(obs.shape)))
     if obs.dtype != torch.float32 or not obs.is_cuda:
         raise TypeError("obs must be a float32 device tensor")
+    if (obs.dim() == 3 and not obs.is_contiguous() and obs.stride(-1) == 1 and obs.shape[0] > 0 and obs.shape[1] > 0
+            and obs.stride(1) >= OBS_DIM and obs.stride(0) >= (obs.shape[1] - 1) * obs.stride(1) + OBS_DIM):
+        # a strided (B, K, 15) stack -- e.g. F16Envs(obs_layout="window")'s observation view --
+        # read in place by f16env_features_strided
+        B, K = obs.shape[0], obs.shape[1]
+        if out is None:
+            out = torch.empty((B, K, FEATURES_DIM), dtype=torch.float32, device=obs.device)
+        elif tuple(out.shape) != (B, K, FEATURES_DIM) or not out.is_contiguous() or out.dtype != torch.float32:
+            raise ValueError("out must be a contiguous float32 tensor of shape %s" % ((B, K, FEATURES_DIM),))
+        stream = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        check(lib().f16env_features_strided(stream, B, K, ctypes.c_void_p(obs.data_ptr()), obs.stride(0), obs.stride(1),
+                                            ctypes.c_void_p(out.data_ptr())), "f16env_features_strided")
+        return out
     obs = obs.contiguous()
     n = obs.numel() // OBS_DIM
     if out is None:

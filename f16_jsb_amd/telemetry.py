@@ -27,9 +27,11 @@ def poses(obs: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     if obs.dtype != torch.float32 or not obs.is_cuda:
         raise TypeError("obs must be a float32 device tensor")
     if obs.dim() == 3 and obs.shape[-1] == 15:
-        obs = obs.contiguous()
+        if obs.stride(-1) != 1 or obs.shape[0] == 0 or obs.stride(0) < 15:
+            obs = obs.contiguous()
+        # the newest frame of each stack read in place (contiguous or windowed layout)
         n, k = obs.shape[0], obs.shape[1]
-        base, stride = obs.data_ptr() + 4 * 15 * (k - 1), 15 * k
+        base, stride = obs.data_ptr() + 4 * obs.stride(1) * (k - 1), obs.stride(0)
     elif obs.dim() == 2 and obs.shape[-1] == 15:
         obs = obs.contiguous()
         n, base, stride = obs.shape[0], obs.data_ptr(), 15

@@ -209,11 +209,12 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
 /* Windowed observations: the same env step without the stack shift copy (the "state-stacking
  * ring buffer" of BASELINE.json north_star: JSBSimEnv's `obs_buffer` deque(maxlen=K),
  * jsbsim_gym.py:150 and its append at :235, and DummyVecEnv's stacked obs buffer,
- * dummy_vec_env.py:56-73). The caller owns two frame histories of T frames per env,
- * hist[b] = N x T x 15 float (T % 4 == 0, T >= 2K). The observation of a step is the window
- *     hist_cur[k][pos-K+1 .. pos][0..15)      (a strided N x K x 15 view: strides T*15, 15, 1)
- * with identical values to f16env_step's obs. A step writes only its new frame, at `pos` of
- * both histories (reset lanes also fill their window), alternating hist_cur / hist_other
+ * dummy_vec_env.py:56-73). The caller owns two frame histories of T frame slots per env,
+ * hist[b] = N x T x 16 float (a 15-float frame + one 0 per 64-B slot; T >= 2K).
+ * The observation of a step is the window
+ *     hist_cur[k][pos-K+1 .. pos][0..15)      (a strided N x K x 15 view: strides T*16, 16, 1)
+ * with identical values to f16env_step's obs. A step writes only its new frame, one whole
+ * 64-B slot at `pos` of both histories (reset lanes also fill their window), alternating hist_cur / hist_other
  * between steps (pos advancing by one); the terminal observation of a lane that finished is
  * the same window of hist_other (no copy; valid until the next step, like terminal_obs).
  * The other parity's window is not written, so an observation stays valid until the step
@@ -311,6 +312,12 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
  *        with d = |goal - pos|_xy, dz = goal_z - h, rb = atan2(dy, dx) - psi.
  * No handle needed; stream-ordered. */
 int f16env_features(void* stream, int64_t n_frames, const float* obs, float* feat);
+
+/* f16env_features on a strided (B, K, 15) block: frame (b, k) at obs + b*row_stride +
+ * k*frame_stride (floats), e.g. a windowed observation read in place (row_stride T*16,
+ * frame_stride 16); feat is (B, K, 17) contiguous. */
+int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float* obs, int64_t row_stride,
+                            int64_t frame_stride, float* feat);
 
 /* Render/telemetry poses, replacing the state -> Viewer transform of
  * jsbsim_gym.py:381-415 (JSBSimEnv.render) for every env at once, float32:

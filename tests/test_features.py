@@ -115,6 +115,36 @@ def test_gpu_features_of_env_obs(gpu):
     e.close()
 
 
+@pytest.mark.gpu
+def test_gpu_features_of_window_view(gpu):
+    """The transform read in place from a windowed observation (strided (N, K, 15) view,
+    f16env_features_strided) equals the transform of the same frames made contiguous, and
+    the reference transform; plus an odd-stride (unaligned) slice."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.features import stacked_features
+    e = F16Envs(1000, stack_k=4, seed=5, obs_layout="window", history=12)
+    e.reset()
+    for t in range(20):
+        out = e.step(e.sample_actions(2, t))
+    assert not out.obs.is_contiguous()
+    a = stacked_features(out.obs)
+    b = stacked_features(out.obs.contiguous())
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    _check(a, stacked_features_ref(out.obs.cpu()))
+    big = torch.randn(300, 7, 19, device="cuda") * 100
+    v = big[:, 1:6, 2:17]  # row stride 133, frame stride 19, 8-B-misaligned base
+    torch.testing.assert_close(stacked_features(v), stacked_features(v.contiguous()), rtol=0, atol=0)
+    e.close()
+
+
+def test_default_history_is_4_times_odd():
+    from f16_jsb_amd.env import _default_history
+    for k in (1, 4, 10, 62, 63, 100, 200):
+        T = _default_history(k)
+        assert T >= 2 * k and T % 4 == 0 and (T // 4) % 2 == 1 and T >= 124
+
+
 def test_features_rejects_bad_input():
     from f16_jsb_amd.features import features
     with pytest.raises(ValueError):

@@ -132,13 +132,14 @@ def test_window_set_state_and_obs(gpu):
 
 
 def test_window_views_and_layout(gpu):
-    """The observation is a strided view: (N, K, 15), strides (T*15, 15, 1), flattenable to
-    (N, K*15) without a copy; the rollout entry points refuse the window layout."""
+    """The observation is a strided view of 64-B frame slots: (N, K, 15), strides (T*16, 16, 1),
+    the slots' 16th float 0; the rollout entry points refuse the window layout."""
     from f16_jsb_amd.env import F16EnvError, F16Envs
     e = F16Envs(64, stack_k=4, seed=1, obs_layout="window", history=16)
     o = e.reset()
-    assert tuple(o.shape) == (64, 4, 15) and o.stride() == (16 * 15, 15, 1)
-    flat = o.reshape(64, 60)
-    assert flat.data_ptr() == o.data_ptr()
+    assert tuple(o.shape) == (64, 4, 15) and o.stride() == (16 * 16, 16, 1)
+    for t in range(1, 30):  # across a restart
+        e.step(e.sample_actions(1, t))
+    assert float(e._hist[..., 15].abs().max()) == 0.0
     with pytest.raises(F16EnvError):
         e.rollout_random(0, 0, 2, None, None, None, None, None)

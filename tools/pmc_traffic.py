@@ -34,7 +34,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--stack", type=int, default=4)
-    ap.add_argument("--kernel", default="f16_step_kernel")
+    ap.add_argument("--kernel", default="f16_step_win_kernel")
+    ap.add_argument("--layout", default="window", choices=("window", "contiguous"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     from f16_jsb_amd._lib import lib
@@ -44,9 +45,9 @@ def main():
     rd = 2.0 * fetch_kib * 1024.0
     wr = write_kib * 1024.0
     state_bytes = int(lib().f16env_state_bytes_per_env())
-    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes) * a.envs
+    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes, a.layout) * a.envs
     d = {
-        "kernel": a.kernel, "envs": a.envs, "stack_k": a.stack, "state_bytes": state_bytes,
+        "kernel": a.kernel, "layout": a.layout, "envs": a.envs, "stack_k": a.stack, "state_bytes": state_bytes,
         "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib, "launches": [nf, nw],
         "hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
         "hbm_bytes_per_launch": int(rd + wr),

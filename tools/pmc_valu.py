@@ -31,7 +31,7 @@ def main():
     ap.add_argument("inputs", nargs="+")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--stack", type=int, default=4)
-    ap.add_argument("--kernel", default="f16_step_kernel")
+    ap.add_argument("--kernel", default="f16_step_win_kernel")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     vals = collections.defaultdict(list)
