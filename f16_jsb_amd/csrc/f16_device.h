@@ -189,11 +189,19 @@ struct Lane {
   int32_t step, ep_count, flags;
 };
 
+// The halves of a double for the state columns. The empty asm pins the double in a register
+// pair first: without it the optimiser narrows "load double; take the low/high word" into two
+// 4-byte loads, SROA then cannot promote the Lane's fp64 members (mixed double / float accesses
+// of one slot), and they lived in scratch for the whole kernel (72 B per lane, r02).
 __device__ __forceinline__ double f2d(float lo, float hi) {
-  return __hiloint2double(__float_as_int(hi), __float_as_int(lo));
+  return __builtin_bit_cast(double, ((uint64_t)__float_as_uint(hi) << 32) | __float_as_uint(lo));
 }
-__device__ __forceinline__ float dlo(double d) { return __int_as_float(__double2loint(d)); }
-__device__ __forceinline__ float dhi(double d) { return __int_as_float(__double2hiint(d)); }
+__device__ __forceinline__ uint64_t dbits(double d) {
+  asm("" : "+v"(d));
+  return __builtin_bit_cast(uint64_t, d);
+}
+__device__ __forceinline__ float dlo(double d) { return __uint_as_float((uint32_t)dbits(d)); }
+__device__ __forceinline__ float dhi(double d) { return __uint_as_float((uint32_t)(dbits(d) >> 32)); }
 // a flag bit carried in the sign of a non-negative float
 __device__ __forceinline__ float with_sign_flag(float v, bool f) {
   return __uint_as_float((__float_as_uint(v) & 0x7fffffffu) | (f ? 0x80000000u : 0u));
@@ -230,6 +238,11 @@ __device__ __forceinline__ void latch_from_state(Lane& L) {
   L.lx[F16L_VG_FPS] = ground_speed((float)(L.vI[0] + w * L.rI[1]), (float)(L.vI[1] - w * L.rI[0]), (float)L.vI[2],
                                    (float)L.rI[0], (float)L.rI[1], (float)L.rI[2]);
 }
+
+// 16-B output store of the step kernels (state columns, history frame slots): plain
+// global_store_dwordx4. Write-through (buffer store sc1) and non-temporal forms were measured
+// slower, the window layout's 64-B slot writes up to 2x (profiles/r02_variants_store.json).
+__device__ __forceinline__ void st16(float4* p, float4 v) { *p = v; }
 
 template <bool GUST>
 __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, float4 g, Lane& L) {
@@ -312,10 +325,10 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n)
-    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) *p = c[j];
+    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) st16(p, c[j]);
   if (GUST && PART != 2) {
-    *p = make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f);
-    *(p + n) = make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f);
+    st16(p, make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f));
+    st16(p + n, make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f));
   }
 }
 

@@ -497,10 +497,10 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 static constexpr int WPITCH = 16;  // floats per history frame slot
 __device__ __forceinline__ void put_slot(float* d, const float* f) {
   float4* q = reinterpret_cast<float4*>(d);
-  q[0] = make_float4(f[0], f[1], f[2], f[3]);
-  q[1] = make_float4(f[4], f[5], f[6], f[7]);
-  q[2] = make_float4(f[8], f[9], f[10], f[11]);
-  q[3] = make_float4(f[12], f[13], f[14], 0.0f);
+  st16(q, make_float4(f[0], f[1], f[2], f[3]));
+  st16(q + 1, make_float4(f[4], f[5], f[6], f[7]));
+  st16(q + 2, make_float4(f[8], f[9], f[10], f[11]));
+  st16(q + 3, make_float4(f[12], f[13], f[14], 0.0f));
 }
 static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([4][64] float4)
 
