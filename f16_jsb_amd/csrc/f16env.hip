@@ -719,8 +719,33 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * WPITCH, f0);
     }
     // this step's frame at position p of both histories (wx: the reset frame of a lane reset
-    // now, else the new frame; wy: the new frame), aligned stores at the uniform phase
-    if (live) {
+    // now, else the new frame; wy: the new frame). A full wave transposes its 64 slots through
+    // its LDS staging area so that each dwordx4 store instruction writes 16 whole 64-B slots
+    // (4 lanes per slot) instead of one 16-B quarter of 64 slots: a quarter of the cache lines
+    // touched per store instruction. Swizzle: quarter j of slot r at float4 r*4 + (j ^ (r>>2 & 3)),
+    // conflict-free on both the per-lane writes and the per-slot reads.
+    if (rows == 64) {
+      float4* st4 = reinterpret_cast<float4*>(stg);
+      const int q = lane & 3, sw = (lane >> 2) & 3;
+      float* const hist[2] = {a.wx, a.wy};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* fr = (h == 0 && reset_now) ? f0 : f;
+        __builtin_amdgcn_wave_barrier();
+        st4[lane * 4 + (0 ^ sw)] = make_float4(fr[0], fr[1], fr[2], fr[3]);
+        st4[lane * 4 + (1 ^ sw)] = make_float4(fr[4], fr[5], fr[6], fr[7]);
+        st4[lane * 4 + (2 ^ sw)] = make_float4(fr[8], fr[9], fr[10], fr[11]);
+        st4[lane * 4 + (3 ^ sw)] = make_float4(fr[12], fr[13], fr[14], 0.0f);
+        __builtin_amdgcn_wave_barrier();
+        float* dst = hist[h] + (row0 + (lane >> 2)) * a.wrow + (int64_t)p * WPITCH + 4 * q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * j + (lane >> 2);
+          st16(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wrow), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else if (live) {
       const int64_t off = k * a.wrow + (int64_t)p * WPITCH;
       put_slot(a.wx + off, reset_now ? f0 : f);
       put_slot(a.wy + off, f);
@@ -967,7 +992,10 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
     double ce, se;
     earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);
-    for (int s = 0; s < a.E.down_sample; ++s) frame<false, false>(L, cmd, ce, se, A, sT, a.C, false);  // :225-232
+#ifdef F16_STAMPS
+    Stamps stamps = {};
+#endif
+    for (int s = 0; s < a.E.down_sample; ++s) frame<false, false>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
     float f[F16_OBS_DIM];
     make_frame(L, ce, se, A, f);                              // :234
     float r32;

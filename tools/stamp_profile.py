@@ -19,10 +19,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--stack", type=int, default=4)
+    ap.add_argument("--layout", default="window", choices=("window", "contiguous"))
+    ap.add_argument("--build-only", action="store_true")
     args = ap.parse_args()
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
-                    "-DF16_STAMPS", "-shared", "-fPIC", "-Wno-unused-value", "-fno-slp-vectorize",
-                    os.path.join(ROOT, "f16_jsb_amd", "csrc", "f16env.hip"), "-o", DIAG], check=True)
+    src = os.path.join(ROOT, "f16_jsb_amd", "csrc")
+    fresh = os.path.exists(DIAG) and all(os.path.getmtime(os.path.join(src, f)) <= os.path.getmtime(DIAG)
+                                         for f in os.listdir(src))
+    if not fresh:  # build here (CPU container) beforehand; the box then reuses it
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I",
+                        os.path.join(ROOT, "include"), "-DF16_STAMPS", "-shared", "-fPIC", "-Wno-unused-value",
+                        "-fno-slp-vectorize", os.path.join(src, "f16env.hip"), "-o", DIAG], check=True)
+    if "--build-only" in sys.argv:
+        return
     os.environ["F16ENV_LIB"] = DIAG
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -31,7 +39,8 @@ def main():
     from f16_jsb_amd.env import F16Envs
     L = _lib.lib()
     L.f16env_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    e = F16Envs(args.envs, stack_k=args.stack, seed=1)
+    e = F16Envs(args.envs, stack_k=args.stack, seed=1, obs_layout=args.layout)
+    print("kernel", e.step_kernel_name)
     e.reset()
     for t in range(30):
         e.step(e.sample_actions(3, t))
