@@ -132,7 +132,6 @@ static constexpr double J2_E = 1.08262982e-03;
 static constexpr double OMEGA_E = 0.00007292115;
 static constexpr double E2 = 1.0 - (WGS_B * WGS_B) / (WGS_A * WGS_A);
 static constexpr double EC2 = 1.0 - E2;
-static constexpr double ELL_C = WGS_A * E2;
 static constexpr float S_W = 300.0f, B_W = 30.0f, CBAR = 11.32f;
 static constexpr float PI_F = 3.14159265358979323846f;
 static constexpr double PI_D = 3.14159265358979323846;
@@ -635,34 +634,50 @@ __device__ __forceinline__ void cross_c(const float* a, const float* b, float* o
   o[2] = term(a[0], b[1], a[1], b[0]);
 }
 
-// Geodetic altitude from ECEF (Fukushima 2006, one Halley step; FGLocation), fp64, plus
-// the geodetic surface normal (for the per-step altitude reference below).
+// Geodetic altitude from ECEF (FGLocation's geodetic altitude), plus the geodetic surface
+// normal (for the per-step altitude reference below). The latitude comes from Bowring's
+// formula in fp32; the altitude is then h = p cos(lat) + |z| sin(lat) - a sqrt(1 - e^2 sin^2)
+// in fp64, which is STATIONARY in the latitude at the true geodetic latitude, so the fp32
+// latitude error (~1e-7 rad) enters only quadratically (R * 1e-14 ~ 1e-6 ft). fp64 pieces:
+// p = |(x, y)| and the ellipsoid root by one Newton step from fp32 seeds, (cos, sin) renormalised
+// to a unit pair (an off-unit pair would err linearly, ~R * 6e-8). Worst error vs the exact
+// geodetic altitude over latitudes +-90 deg and -2 000 .. 120 000 ft: 7.4e-7 ft (numpy emulation
+// of these operations; the fp32 observation resolves 1e-3 ft). ~16 fp64 instructions instead of
+// the ~120 of an fp64 Fukushima step with its four fp64 square roots and a division.
 struct AltRef {
   double r0[3];  // ECEF position where h0 was evaluated exactly
   double h0;
   float n[3];    // geodetic up-normal there
 };
 __device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRef& A) {
-  const double rxy = sqrt(x * x + y * y);
-  const double ec = WGS_B / WGS_A;
+  constexpr double EP2 = (WGS_A * WGS_A) / (WGS_B * WGS_B) - 1.0;
+  const double p2 = x * x + y * y;
+  const float r0 = p2 > 0.0 ? __builtin_amdgcn_rsqf((float)p2) : 0.0f;
+  const double p0 = p2 * (double)r0;
+  const double p = __builtin_fma((double)(0.5f * r0), __builtin_fma(-p0, p0, p2), p0);
   const double s0 = fabs(z);
-  const double zc = ec * s0, c0 = ec * rxy;
-  const double c02 = c0 * c0, s02 = s0 * s0;
-  const double a02 = c02 + s02, a0 = sqrt(a02), a03 = a02 * a0;
-  double s1 = zc * a03 + ELL_C * s02 * s0;
-  const double c1 = rxy * a03 - ELL_C * c02 * c0;
-  const double cs0c0 = ELL_C * c0 * s0;
-  const double b0 = 1.5 * cs0c0 * ((rxy * s0 - zc * c0) * a0 - cs0c0);
-  s1 = s1 * a03 - b0 * s0;
-  const double cc = ec * (c1 * a03 - b0 * c0);
-  const double s12 = s1 * s1, cc2 = cc * cc;
-  const double norm = sqrt(s12 + cc2);
-  const double inv = 1.0 / norm;
-  A.h0 = (rxy * cc + s0 * s1 - WGS_A * sqrt(EC2 * s12 + cc2)) * inv;
-  const float cl = (float)(cc * inv), sl = (float)(s1 * inv) * (z < 0.0 ? -1.0f : 1.0f);
+  const float pf = (float)p, zf = (float)s0;
+  // Bowring: parametric latitude, then the geodetic one, as unit (cos, sin) pairs
+  const float u = zf * (float)WGS_A, v = pf * (float)WGS_B;
+  const float ri = __builtin_amdgcn_rsqf(u * u + v * v);
+  const float st = u * ri, ct = v * ri;
+  const float num = zf + (float)(EP2 * WGS_B) * (st * st * st);
+  const float den = pf - (float)(E2 * WGS_A) * (ct * ct * ct);
+  const float r2 = __builtin_amdgcn_rsqf(num * num + den * den);
+  const float slf = num * r2, clf = den * r2;
+  double c = clf, sn = slf;
+  const double k = __builtin_fma(-0.5, __builtin_fma(c, c, sn * sn), 1.5);
+  c *= k;
+  sn *= k;
+  const double w = __builtin_fma(-E2 * sn, sn, 1.0);
+  const float sw0 = __builtin_amdgcn_sqrtf((float)w);
+  const double swd = sw0;
+  const double sw = __builtin_fma((double)(0.5f * __builtin_amdgcn_rcpf(sw0)), __builtin_fma(-swd, swd, w), swd);
+  A.h0 = __builtin_fma(p, c, __builtin_fma(s0, sn, -WGS_A * sw));
+  const float cl = clf, sl = slf * (z < 0.0 ? -1.0f : 1.0f);
   float clon = 1.0f, slon = 0.0f;
-  if (rxy != 0.0) {
-    const float ir = __builtin_amdgcn_rcpf((float)rxy);
+  if (pf != 0.0f) {
+    const float ir = __builtin_amdgcn_rcpf(pf);
     clon = (float)x * ir;
     slon = (float)y * ir;
   }
@@ -672,7 +687,7 @@ __device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRe
 
 // Everything FGPropagate / FGInertial derive from the integrated state.
 // ce, se: cos/sin of the Earth position angle (fp64).
-// The geodetic altitude is evaluated exactly (fp64 Fukushima) once per env step (AltRef) and
+// The geodetic altitude is evaluated (alt_ref_init, ~1e-6 ft) once per env step (AltRef) and
 // advanced within the step along the geodetic normal: h = h0 + n . (rE - r0). Over one env
 // step |rE - r0| < 70 ft, so the neglected curvature term |dr|^2/2R < 2e-4 ft (far below the
 // 4e-4 ft fp32 resolution of the observed altitude).

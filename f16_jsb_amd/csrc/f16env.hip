@@ -458,10 +458,10 @@ struct StepArgs {
   float* r_rew;                // N: rewards
   float* r_next_start;         // N: done as 0/1 float (episode_starts of the next slot)
   // windowed observations (f16env_step_window): the frame histories of this step (wx, the one
-  // whose window is the returned observation) and of the other parity (wy), [N][T][15] each
+  // whose window is the returned observation) and of the other parity (wy), [N][T][16] each
   float* wx;
   float* wy;
-  int64_t wrow;                // floats per env row = T * 15
+  int64_t wrow;                // floats per env row = T * 16
   int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
   EnvArgs E;
   ModelConsts C;
