@@ -458,10 +458,12 @@ struct StepArgs {
   float* r_rew;                // N: rewards
   float* r_next_start;         // N: done as 0/1 float (episode_starts of the next slot)
   // windowed observations (f16env_step_window): the frame histories of this step (wx, the one
-  // whose window is the returned observation) and of the other parity (wy), [N][T][16] each
+  // whose window is the returned observation) and of the other parity (wy), [T][N][16] each
+  // (position-major: the N slots of one position are contiguous)
   float* wx;
   float* wy;
-  int64_t wrow;                // floats per env row = T * 16
+  int64_t wrow;                // floats between positions (position-major: N * 16; env-major: 16)
+  int64_t wenv;                // floats between envs (position-major: 16; env-major: T * 16)
   int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
   EnvArgs E;
   ModelConsts C;
@@ -482,9 +484,9 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // GT: tables read from the global blob (L1/L2-resident, 12 KB) instead of an LDS copy, which
 // frees the LDS for the stack image at large K (K = 10: four 38.5 KB images + the blob exceed
 // 160 KB). sT is then unused.
-// Windowed observations (WIN, f16env_step_window): per env two frame histories [T][16] (wx:
-// this step's parity, wy: the other; 16-float = 64-B frame slots, the 16th float 0), the
-// observation of a step being the view wx[k][p-K+1 .. p][0..15) (strides T*16, 16, 1). A step
+// Windowed observations (WIN, f16env_step_window): two frame histories [T][N][16] (wx: this
+// step's parity, wy: the other; position-major 16-float = 64-B frame slots, the 16th float 0),
+// the observation of a step being the view wx[p-K+1 .. p][k][0..15) (strides 16, N*16, 1). A step
 // writes its new frame at position p of BOTH histories -- no stack shift copy, no
 // previous-stack read -- as four aligned 16-B stores filling one whole 64-B sector (a 60-B
 // frame at a 60-B pitch leaves partial sectors, which cost as much as the whole-row rewrite
@@ -569,7 +571,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     L.flags &= ~LANE_FLAG_FRESH;
   }
   if (WIN && fresh && a.E.K > 1) {
-    const float* src = a.wy + k * a.wrow + (int64_t)(a.wpos - 1) * WPITCH;
+    const float* src = a.wy + k * a.wenv + (int64_t)(a.wpos - 1) * a.wrow;
 #pragma unroll
     for (int j = 0; j < 4; ++j) dma16(src + 4 * j, stg + j * 256);  // [j][lane] float4
   }
@@ -705,7 +707,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     const int K = a.E.K, p = a.wpos;
     const bool reset_now = live && done && autoreset;
     if (live && K > 1 && (fresh || reset_now)) {  // rare: whole-window fills of reset lanes
-      float* X = a.wx + k * a.wrow;
+      float* X = a.wx + k * a.wenv;
       if (fresh) {
         float f0p[16];
 #pragma unroll
@@ -713,16 +715,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
           const float4 v = reinterpret_cast<const float4*>(stg)[j * 64 + lane];
           f0p[4 * j] = v.x; f0p[4 * j + 1] = v.y; f0p[4 * j + 2] = v.z; f0p[4 * j + 3] = v.w;
         }
-        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * WPITCH, f0p);
+        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * a.wrow, f0p);
       }
       if (reset_now)  // after the fresh fill: a one-step episode ends in its own reset window
-        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * WPITCH, f0);
+        for (int r = p - K + 1; r < p; ++r) put_slot(X + (int64_t)r * a.wrow, f0);
     }
     // this step's frame at position p of both histories (wx: the reset frame of a lane reset
-    // now, else the new frame; wy: the new frame). A full wave transposes its 64 slots through
-    // its LDS staging area so that each dwordx4 store instruction writes 16 whole 64-B slots
-    // (4 lanes per slot) instead of one 16-B quarter of 64 slots: a quarter of the cache lines
-    // touched per store instruction. Swizzle: quarter j of slot r at float4 r*4 + (j ^ (r>>2 & 3)),
+    // now, else the new frame; wy: the new frame). The wave's 64 slots are one contiguous
+    // 4 KiB block; the wave transposes them through its LDS staging area so that each dwordx4
+    // store instruction writes 1 KiB contiguous (16 whole slots, 4 lanes per slot) instead of a
+    // 16-B quarter of every slot. Swizzle: quarter j of slot r at float4 r*4 + (j ^ (r>>2 & 3)),
     // conflict-free on both the per-lane writes and the per-slot reads.
     if (rows == 64) {
       float4* st4 = reinterpret_cast<float4*>(stg);
@@ -737,16 +739,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         st4[lane * 4 + (2 ^ sw)] = make_float4(fr[8], fr[9], fr[10], fr[11]);
         st4[lane * 4 + (3 ^ sw)] = make_float4(fr[12], fr[13], fr[14], 0.0f);
         __builtin_amdgcn_wave_barrier();
-        float* dst = hist[h] + (row0 + (lane >> 2)) * a.wrow + (int64_t)p * WPITCH + 4 * q;
+        float* dst = hist[h] + (int64_t)p * a.wrow + (row0 + (lane >> 2)) * a.wenv + 4 * q;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 16 * j + (lane >> 2);
-          st16(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wrow), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
+          st16(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wenv), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
         }
       }
       __builtin_amdgcn_wave_barrier();
     } else if (live) {
-      const int64_t off = k * a.wrow + (int64_t)p * WPITCH;
+      const int64_t off = k * a.wenv + (int64_t)p * a.wrow;
       put_slot(a.wx + off, reset_now ? f0 : f);
       put_slot(a.wy + off, f);
     }
@@ -1042,10 +1044,11 @@ struct ResetDoneArgs {
   SoA s, tmpl;
   const int32_t* done_idx;
   const int32_t* n_done;
-  float* obs;       // row of env k: obs + k * obs_row + obs_off, frames obs_pitch floats apart
-                    // (contiguous: K*15, 0, 15; window: T*16, (p-K+1)*16, 16)
-  int64_t obs_row, obs_off;
-  int32_t obs_pitch;
+  float* obs;       // frame r of env k at obs + k * obs_row + obs_off + r * obs_pitch, obs_slot
+                    // floats written per frame (contiguous: K*15, 0, 15, 15; window:
+                    // 16, (p-K+1)*N*16, N*16, 16)
+  int64_t obs_row, obs_off, obs_pitch;
+  int32_t obs_slot;
   EnvArgs E;
   ModelConsts C;
 };
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
     lane_store<true>(a.s, k, L);
     float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
-      for (int j = 0; j < a.obs_pitch; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
+      for (int j = 0; j < a.obs_slot; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
   }
 }
 
@@ -1073,9 +1076,9 @@ struct ResetArgs {
   const uint8_t* mask;
   const float* goals;
   const double* ic;
-  float* obs;       // row addressing as ResetDoneArgs
-  int64_t obs_row, obs_off;
-  int32_t obs_pitch;
+  float* obs;       // frame addressing as ResetDoneArgs
+  int64_t obs_row, obs_off, obs_pitch;
+  int32_t obs_slot;
   int* wind_any;    // per-lane IC given: set if a lane got wind (the handle needs the wind kernels)
   EnvArgs E;
   ModelConsts C;
@@ -1099,20 +1102,23 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_kernel(ResetArgs a) {
   if (a.obs) {
     float* o = a.obs + k * a.obs_row + a.obs_off;
     for (int r = 0; r < a.E.K; ++r)
-      for (int j = 0; j < a.obs_pitch; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
+      for (int j = 0; j < a.obs_slot; ++j) o[r * a.obs_pitch + j] = j < F16_OBS_DIM ? f0[j] : 0.0f;
   }
 }
 
-// windowed observations: the histories' last K-1 frames (positions p_old-K+2 .. p_old) move
-// to the front (0 .. K-2) of both histories, so the next step writes its frame at K-1
-__global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wrow, int32_t p_old, float* h0, float* h1) {
-  const int64_t per = (int64_t)(K - 1) * WPITCH;
+// windowed observations: the histories' last K-1 frame positions (p_old-K+2 .. p_old) move to
+// the front (0 .. K-2) of both histories, so the next step writes its frame at K-1. One lane
+// per float4 of a slot; (wenv, wpos) as StepArgs (wrow, wenv).
+__global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wenv, int64_t wpos, int32_t p_src, float* h0,
+                                          float* h1) {
+  const int64_t per = (int64_t)(K - 1) * n * 4;  // float4 per history
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * n * per) return;
-  const int64_t b = i / (n * per), r = i - b * n * per;
-  const int64_t k = r / per, j = r - k * per;
-  float* row = (b ? h1 : h0) + k * wrow;
-  row[j] = row[(int64_t)(p_old - K + 2) * WPITCH + j];
+  if (i >= 2 * per) return;
+  const int64_t b = i >= per, t = i - b * per;
+  const int64_t q = t & 3, u = t >> 2;
+  const int64_t k = u % n, r = u / n;  // position-major order: consecutive lanes, consecutive envs
+  float* d = (b ? h1 : h0) + k * wenv + r * wpos + 4 * q;
+  *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(d + (int64_t)p_src * wpos);
 }
 
 // IC -> state (used once at create to build the reset template, n = 1)
@@ -1361,7 +1367,8 @@ __global__ __launch_bounds__(256) void f16_features_kernel(int64_t n_frames, con
 }
 
 // The same per-frame transform on a strided (B, K, 15) block -- e.g. a windowed observation
-// (rows T*16 floats apart, 64-B frame slots) read in place, no copy to a contiguous stack.
+// (env rows 16 floats apart, frames N*16 apart: position-major 64-B slots) read in place, no
+// copy to a contiguous stack.
 // One lane per frame (16-B vector reads of its slot when the strides allow); the (B, K, 17)
 // output leaves through LDS as coalesced float4, as in f16_features_kernel.
 __global__ __launch_bounds__(256) void f16_features_strided_kernel(int64_t n_rows, int32_t K, const float* __restrict__ obs,
@@ -1453,6 +1460,7 @@ struct f16env {
                       // steady wind: config / random-IC box / set_state)
   int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
   int win_occ;        // the same for the windowed-observation step kernel
+  int win_env_major;  // window histories [N][T][16] (1) instead of the default [T][N][16] (0)
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
@@ -1727,6 +1735,7 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   ResetArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = obs;
   a.obs_row = (int64_t)h->cfg.stack_k * F16_OBS_DIM; a.obs_off = 0; a.obs_pitch = F16_OBS_DIM;
+  a.obs_slot = F16_OBS_DIM;
   a.E = env_args(h);
   a.C = h->C;
   return reset_launch(h, (hipStream_t)stream, a);
@@ -1754,7 +1763,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   float* feat = slot ? slot->features : nullptr;
   if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
     return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
-  a.wx = a.wy = nullptr; a.wrow = 0; a.wpos = 0;
+  a.wx = a.wy = nullptr; a.wrow = a.wenv = 0; a.wpos = 0;
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = h->lds_image;
@@ -1778,7 +1787,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = obs;
-    r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0; r.obs_pitch = F16_OBS_DIM;
+    r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0; r.obs_pitch = F16_OBS_DIM; r.obs_slot = F16_OBS_DIM;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1798,6 +1807,18 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
                 int32_t* done_idx, int32_t* n_done) {
   return step_impl(h, stream, nullptr, act, obs_prev, obs, rew, terminated, truncated, terminal_obs, ep_return,
                    ep_len, done_idx, n_done);
+}
+
+// (floats between positions, floats between envs) of the handle's window history order
+static void window_strides(f16env_t h, int64_t T, int64_t& wpos, int64_t& wenv) {
+  if (h->win_env_major) { wpos = WPITCH; wenv = T * WPITCH; }
+  else { wpos = (int64_t)h->cfg.n_envs * WPITCH; wenv = WPITCH; }
+}
+
+int f16env_set_window_order(f16env_t h, int env_major) {
+  if (!h) return set_err(-1, "null handle");
+  h->win_env_major = env_major ? 1 : 0;
+  return 0;
 }
 
 static int window_check(f16env_t h, const float* hist_cur, const float* hist_other, int64_t T, int32_t pos) {
@@ -1826,7 +1847,9 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   a.term = terminated; a.trunc = truncated; a.ep_ret = ep_return; a.ep_len = ep_len;
   a.done_idx = done_idx; a.n_done = n_done;
   a.nonfinite = h->nonfinite;
-  a.wx = hist_cur; a.wy = hist_other; a.wrow = T * WPITCH; a.wpos = pos;
+  int64_t P, Q;  // floats between positions, between envs
+  window_strides(h, T, P, Q);
+  a.wx = hist_cur; a.wy = hist_other; a.wrow = P; a.wenv = Q; a.wpos = pos;
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = 0;
@@ -1848,7 +1871,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
-    r.obs_row = T * WPITCH; r.obs_off = (int64_t)(pos - a.E.K + 1) * WPITCH; r.obs_pitch = WPITCH;
+    r.obs_row = Q; r.obs_off = (int64_t)(pos - a.E.K + 1) * P; r.obs_pitch = P; r.obs_slot = WPITCH;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1863,7 +1886,9 @@ int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const flo
   if (int e = window_check(h, hist_cur, nullptr, T, pos)) return e;
   ResetArgs a;
   a.s = h->soa; a.tmpl = h->tmpl; a.mask = mask; a.goals = goals; a.ic = ic; a.obs = hist_cur;
-  a.obs_row = T * WPITCH; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * WPITCH; a.obs_pitch = WPITCH;
+  int64_t P, Q;
+  window_strides(h, T, P, Q);
+  a.obs_row = Q; a.obs_off = (int64_t)(pos - h->cfg.stack_k + 1) * P; a.obs_pitch = P; a.obs_slot = WPITCH;
   a.E = env_args(h);
   a.C = h->C;
   return reset_launch(h, (hipStream_t)stream, a);
@@ -1876,9 +1901,12 @@ int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, 
   const int K = h->cfg.stack_k;
   if (K < 2) return 0;
   if (pos_old - K + 2 <= K - 2) return set_err(-1, "restart source and destination overlap (pos_old < 2K-3)");
-  const int64_t total = 2 * (int64_t)h->cfg.n_envs * (K - 1) * WPITCH;
-  hipLaunchKernelGGL(f16_window_restart_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, (int64_t)h->cfg.n_envs, (int32_t)K, T * WPITCH, pos_old, hist0, hist1);
+  int64_t P, Q;
+  window_strides(h, T, P, Q);
+  const int64_t blocks = (2 * (int64_t)(K - 1) * h->cfg.n_envs * 4 + 255) / 256;
+  if (blocks > 0x7fffffffLL) return set_err(-1, "history too large for one restart launch");
+  hipLaunchKernelGGL(f16_window_restart_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (int64_t)h->cfg.n_envs, (int32_t)K, Q, P, pos_old - K + 2, hist0, hist1);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1995,8 +2023,7 @@ int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float
   if (n_rows < 0 || K < 1) return set_err(-1, "n_rows >= 0 and K >= 1 required");
   if (n_rows == 0) return 0;
   if (!obs || !feat) return set_err(-1, "null argument");
-  if (frame_stride < F16_OBS_DIM || row_stride < (int64_t)(K - 1) * frame_stride + F16_OBS_DIM)
-    return set_err(-1, "frames overlap (frame_stride >= 15, row_stride >= (K-1) frame_stride + 15)");
+  if (frame_stride < 0 || row_stride < 0) return set_err(-1, "strides must be non-negative");
   if (((uintptr_t)obs & 3) != 0 || ((uintptr_t)feat & 3) != 0) return set_err(-1, "obs and feat must be float-aligned");
   const int64_t blocks = (n_rows * K + 255) / 256;
   if (blocks > 0x7fffffffLL) return set_err(-1, "too many frames");

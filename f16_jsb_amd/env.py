@@ -46,12 +46,8 @@ def _ptr(t) -> Optional[int]:
 
 
 def _default_history(k: int) -> int:
-    """Default window history T: 124 slots (row stride 124 x 64 B = 4 x 31 slots), or the next
-    4 x odd >= 2K for long stacks."""
-    T = 124
-    while T < 2 * k:
-        T += 8
-    return T
+    """Default window history T (positions per history): max(128, 2K)."""
+    return max(128, 2 * k)
 
 
 class F16Envs:
@@ -60,13 +56,13 @@ class F16Envs:
     def __init__(self, n_envs: int, stack_k: int = 10, device=None, seed: int = 0,
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
                  autoreset: bool = True, ic=None, nan_guard: bool = False, obs_layout: str = "contiguous",
-                 history: int = 0, **cfg_kw):
+                 history: int = 0, window_order: str = "position", **cfg_kw):
         """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
-        `history` 64-B frame slots (f16env_step_window: only the new frame is written per step;
-        strides (T*16, 16, 1)); history 0 = 124 or, for K > 62, the next 4 x odd >= 2K (a row
-        stride of 4 x odd 64-B slots spreads the rows over the HBM channels; 127-129 measured
-        slow, profiles/r02_layout_ab.json). Both
+        `history` positions of 64-B frame slots, position-major [T][N][16] (f16env_step_window:
+        only the new frame is written per step, one contiguous block per position; view strides
+        (16, N*16, 1)); history 0 = max(128, 2K) (a restart every T-K+1 steps); window_order
+        "env" keeps the histories env-major [N][T][16] instead (strides (T*16, 16, 1)). Both
         layouts give identical values and the same validity (an observation stays valid until
         the step after next). A consumer that needs a flat (N, K*15) array copies the window
         (reshape); the features kernel (f16_jsb_amd.features) reads it in place."""
@@ -100,8 +96,14 @@ class F16Envs:
             if T < 2 * k:
                 raise ValueError("history must be >= 2 * stack_k")
             self.T = T
-            self._hist = torch.zeros((2, n, T, 16), dtype=f32, device=dev)  # 64-B frame slots
+            if window_order not in ("position", "env"):
+                raise ValueError("window_order must be 'position' or 'env'")
+            self._env_major = window_order == "env"
+            check(L.f16env_set_window_order(h, 1 if self._env_major else 0), "f16env_set_window_order")
+            # [parity][position][env][16] (64-B frame slots, position-major) or [parity][env][position][16]
+            self._hist = torch.zeros((2, n, T, 16) if self._env_major else (2, T, n, 16), dtype=f32, device=dev)
             self._hist_ptr = (self._hist[0].data_ptr(), self._hist[1].data_ptr())
+            self._views = [[None] * T for _ in range(2)]
             self._p = k - 1   # newest frame position of the current observation's window
             self._obs = None
         else:
@@ -139,9 +141,18 @@ class F16Envs:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
     def _window(self, other: int = 0):
-        """(N, K, 15) view of the current (other=0) or other-parity history's window."""
-        p = self._p
-        return self._hist[self._cur ^ other, :, p - self.k + 1:p + 1, :F16_OBS_DIM]
+        """(N, K, 15) view of the current (other=0) or other-parity history's window (views are
+        made once per (parity, position) and reused: a step's host cost stays one ctypes call)."""
+        b, p = self._cur ^ other, self._p
+        v = self._views[b][p]
+        if v is None:
+            v = self._views[b][p] = self._make_window(b, p)
+        return v
+
+    def _make_window(self, b: int, p: int):
+        if self._env_major:
+            return self._hist[b, :, p - self.k + 1:p + 1, :F16_OBS_DIM]
+        return self._hist[b, p - self.k + 1:p + 1, :, :F16_OBS_DIM].transpose(0, 1)
 
     def _no_window(self, what: str):
         if self.window:
@@ -276,12 +287,13 @@ class F16Envs:
         else:
             self._act.copy_(t.as_tensor(actions, dtype=t.float32).reshape(self.n, 4), non_blocking=True)
             act = self._act
-        if tuple(act.shape) != (self.n, 4):
+        if act.shape != (self.n, 4):
             raise ValueError("actions must be (N, 4), got %s" % (tuple(act.shape),))
-        if (done_idx is None) != (n_done is None):
-            raise ValueError("done_idx and n_done go together")
-        self._need(done_idx, (self.n,), t.int32, "done_idx")
-        self._need(n_done, (1,), t.int32, "n_done")
+        if done_idx is not None or n_done is not None:
+            if (done_idx is None) != (n_done is None):
+                raise ValueError("done_idx and n_done go together")
+            self._need(done_idx, (self.n,), t.int32, "done_idx")
+            self._need(n_done, (1,), t.int32, "n_done")
         s = self._stream_int()
         p = self._p + 1
         if p >= self.T:  # move the last K-1 frames to the front of both histories
@@ -393,9 +405,8 @@ class F16Envs:
         next step continues from it)."""
         o = self.torch.as_tensor(obs, dtype=self.torch.float32)
         if self.window:
-            p, k = self._p, self.k
-            self._hist[0, :, p - k + 1:p + 1, :F16_OBS_DIM].copy_(o)
-            self._hist[1, :, p - k + 1:p + 1, :F16_OBS_DIM].copy_(o)
+            self._window(0).copy_(o)
+            self._window(1).copy_(o)
         else:
             self._obs[self._cur].copy_(o)
 

@@ -209,10 +209,10 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
 /* Windowed observations: the same env step without the stack shift copy (the "state-stacking
  * ring buffer" of BASELINE.json north_star: JSBSimEnv's `obs_buffer` deque(maxlen=K),
  * jsbsim_gym.py:150 and its append at :235, and DummyVecEnv's stacked obs buffer,
- * dummy_vec_env.py:56-73). The caller owns two frame histories of T frame slots per env,
- * hist[b] = N x T x 16 float (a 15-float frame + one 0 per 64-B slot; T >= 2K).
- * The observation of a step is the window
- *     hist_cur[k][pos-K+1 .. pos][0..15)      (a strided N x K x 15 view: strides T*16, 16, 1)
+ * dummy_vec_env.py:56-73). The caller owns two frame histories of T positions, position-major,
+ * hist[b] = T x N x 16 float (per env a 15-float frame + one 0: 64-B slots, the N slots of a
+ * position contiguous; T >= 2K). The observation of a step is the window
+ *     hist_cur[pos-K+1 .. pos][k][0..15)      (a strided N x K x 15 view: strides 16, N*16, 1)
  * with identical values to f16env_step's obs. A step writes only its new frame, one whole
  * 64-B slot at `pos` of both histories (reset lanes also fill their window), alternating hist_cur / hist_other
  * between steps (pos advancing by one); the terminal observation of a lane that finished is
@@ -229,6 +229,10 @@ int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const flo
                         float* hist_cur, int64_t T, int32_t pos);
 /* Frames pos_old-K+2 .. pos_old of both histories -> 0 .. K-2 (pos_old = T-1 in practice). */
 int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, int64_t T, int32_t pos_old);
+/* History order of this handle's windowed calls: 0 (default) position-major T x N x 16 as
+ * above; 1 env-major N x T x 16 (view strides T*16, 16, 1). Set before the first windowed call
+ * and keep it: the histories must be laid out accordingly. */
+int f16env_set_window_order(f16env_t h, int env_major);
 /* Waves per SIMD the windowed step kernel of this handle is built for (1 or 2). */
 int f16env_step_window_waves_per_simd(f16env_t h);
 
@@ -314,8 +318,8 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
 int f16env_features(void* stream, int64_t n_frames, const float* obs, float* feat);
 
 /* f16env_features on a strided (B, K, 15) block: frame (b, k) at obs + b*row_stride +
- * k*frame_stride (floats), e.g. a windowed observation read in place (row_stride T*16,
- * frame_stride 16); feat is (B, K, 17) contiguous. */
+ * k*frame_stride (floats, any non-negative strides), e.g. a windowed observation read in
+ * place (row_stride 16, frame_stride N*16); feat is (B, K, 17) contiguous. */
 int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float* obs, int64_t row_stride,
                             int64_t frame_stride, float* feat);
 

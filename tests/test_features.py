@@ -135,14 +135,16 @@ def test_gpu_features_of_window_view(gpu):
     big = torch.randn(300, 7, 19, device="cuda") * 100
     v = big[:, 1:6, 2:17]  # row stride 133, frame stride 19, 8-B-misaligned base
     torch.testing.assert_close(stacked_features(v), stacked_features(v.contiguous()), rtol=0, atol=0)
+    w = big.transpose(0, 1)[:, :, 2:17]  # (7, 300, 15): row stride 19 < frame stride 133
+    torch.testing.assert_close(stacked_features(w), stacked_features(w.contiguous()), rtol=0, atol=0)
     e.close()
 
 
-def test_default_history_is_4_times_odd():
+def test_default_history():
     from f16_jsb_amd.env import _default_history
-    for k in (1, 4, 10, 62, 63, 100, 200):
+    for k in (1, 4, 10, 63, 100, 200):
         T = _default_history(k)
-        assert T >= 2 * k and T % 4 == 0 and (T // 4) % 2 == 1 and T >= 124
+        assert T >= 2 * k and T >= 128
 
 
 def test_features_rejects_bad_input():

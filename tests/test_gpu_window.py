@@ -132,14 +132,25 @@ def test_window_set_state_and_obs(gpu):
 
 
 def test_window_views_and_layout(gpu):
-    """The observation is a strided view of 64-B frame slots: (N, K, 15), strides (T*16, 16, 1),
-    the slots' 16th float 0; the rollout entry points refuse the window layout."""
+    """The observation is a strided view of position-major 64-B frame slots: (N, K, 15), strides
+    (16, N*16, 1), the slots' 16th float 0; the rollout entry points refuse the window layout."""
     from f16_jsb_amd.env import F16EnvError, F16Envs
     e = F16Envs(64, stack_k=4, seed=1, obs_layout="window", history=16)
     o = e.reset()
-    assert tuple(o.shape) == (64, 4, 15) and o.stride() == (16 * 16, 16, 1)
+    assert tuple(o.shape) == (64, 4, 15) and o.stride() == (16, 64 * 16, 1)
     for t in range(1, 30):  # across a restart
         e.step(e.sample_actions(1, t))
     assert float(e._hist[..., 15].abs().max()) == 0.0
     with pytest.raises(F16EnvError):
         e.rollout_random(0, 0, 2, None, None, None, None, None)
+
+
+@pytest.mark.parametrize("k,T", [(4, 8), (1, 4)])
+def test_window_env_major_order(gpu, k, T):
+    """window_order="env" ([N][T][16] histories, view strides (T*16, 16, 1)) against the
+    contiguous layout: the kernel's generic (position, env) slot addressing."""
+    from f16_jsb_amd.env import F16Envs
+    a = F16Envs(700, stack_k=k, seed=7, max_steps=6)
+    b = F16Envs(700, stack_k=k, seed=7, max_steps=6, obs_layout="window", history=T, window_order="env")
+    assert _run(a, b, 40) > 700
+    assert b.obs.stride() == (T * 16, 16, 1)
