@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 def per_launch(d, counter, kernel, grid):
     p = os.path.join(d, "run_counter_collection.csv")
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(p))
-            if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter and int(r["Grid_Size"]) == grid]
+            if r["Kernel_Name"].removeprefix("void ").startswith(kernel) and r["Counter_Name"] == counter and int(r["Grid_Size"]) == grid]
     if not vals:
         raise SystemExit("no %s rows for %s (grid %d) in %s" % (counter, kernel, grid, p))
     return statistics.median(vals), len(vals)

@@ -37,7 +37,7 @@ def main():
     vals = collections.defaultdict(list)
     for p in args.inputs:
         for r in rows(p):
-            if r["Kernel_Name"].startswith(args.kernel) and int(r["Grid_Size"]) == args.envs:
+            if r["Kernel_Name"].removeprefix("void ").startswith(args.kernel) and int(r["Grid_Size"]) == args.envs:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     med = {k: statistics.median(v) for k, v in vals.items()}
     waves = med["SQ_WAVES"]
