@@ -423,10 +423,10 @@ def layout_leg(dev, args, layout, steps=300):
     torch.cuda.synchronize()
     region = s.elapsed_time(en) / steps
     kern_ms, _, _ = e.profile_kernel(lambda: [e.step(acts[t % 16]) for t in range(steps)], steps)
-    b = e.algorithmic_bytes_per_env_step()
+    b, lb = e.stack_bytes_per_env_step(), e.algorithmic_bytes_per_env_step()
     out = {"layout": layout, "kernel": e.step_kernel_name, "region_ms_per_step": round(region, 5),
            "kernel_ms": round(kern_ms, 5), "env_steps_per_s_region": round(args.envs / (region * 1e-3), 1),
-           "algorithmic_bytes_per_env_step": b,
+           "algorithmic_bytes_per_env_step": b, "layout_bytes_per_env_step": lb,
            "frac_of_hbm_peak": round(b * args.envs / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
     e.close()
     return out
@@ -561,8 +561,11 @@ def main():
         return
     total_env_steps = n * world * args.steps
     value = total_env_steps / elapsed
-    bytes_per_env_step = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
-    stack_bytes = envs.stack_bytes_per_env_step() + (24 if cfg5 else 0)
+    # algorithmic bytes: SURVEY.md 8(d)'s per-env-step figure B(K) (the step's contract: state
+    # read + written, action, reward, flags, a K-frame observation); the windowed layout meets
+    # that contract moving fewer bytes (its own count beside it, and the PMC traffic)
+    bytes_per_env_step = envs.stack_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
+    layout_bytes = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)
     bytes_per_launch = bytes_per_env_step * n
     # launch duration used for the roofline: the kernel's average execution time from its own
     # dispatch events (what rocprofv3 --kernel-trace reports); the timed region's GPU time per
@@ -618,12 +621,12 @@ def main():
             "region_ms_per_launch": round(gpu_ms_per_step, 5),
             "region_timing": "HIP events around the timed region on the launch stream / launches",
             "algorithmic_bytes_per_env_step": bytes_per_env_step,
-            "bytes_basis": ("windowed obs: 16 + 2*60 + 4 + 2 + 2S (new frame to both histories; frame "
-                            "slots are 64 B)" if args.obs_layout == "window" else "SURVEY 8(d) B(K)"),
-            # SURVEY 8(d)'s B(K) -- the bytes of the same step with the stack materialised --
-            # over the same launch time: the rate the contiguous layout would need to match it
-            "stack_equivalent_bytes_per_env_step": stack_bytes,
-            "stack_equivalent_frac": round(stack_bytes * n / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "bytes_basis": "SURVEY 8(d) B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S, S = %d" % envs.state_bytes_per_env,
+            # the bytes this layout's kernel must move for the same step (window: the new frame
+            # to both histories, no stack read / rewrite: 16 + 2*60 + 4 + 2 + 2S) and the HBM
+            # fraction they make over the same launch time
+            "layout_bytes_per_env_step": layout_bytes,
+            "layout_frac": round(layout_bytes * n / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
             "obs_layout": args.obs_layout,
             "launch_env_steps": n,
         },

@@ -22,6 +22,10 @@ def time_case(n, k, layout, steps=300, history=0, order="position", ds=4):
     kw = dict(history=history, window_order=order) if layout == "window" else {}
     e = F16Envs(n, stack_k=k, seed=1, obs_layout=layout, down_sample=ds, **kw)
     e.reset()
+    if os.environ.get("F16_AB_SPREAD"):  # bench.py's steady-state episode mix (phase spread + burn-in)
+        import argparse
+        from bench import spread_phases
+        spread_phases(e, argparse.Namespace(seed=0, burn_in=None), e.device)
     acts = [e.sample_actions(5, t) for t in range(16)]
     for t in range(30):
         e.step(acts[t % 16])

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 
 def per_launch(d, counter, kernel, grid):
-    p = os.path.join(d, "run_counter_collection.csv")
+    p = d if d.endswith(".csv") else os.path.join(d, "run_counter_collection.csv")
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(p))
             if r["Kernel_Name"].removeprefix("void ").startswith(kernel) and r["Counter_Name"] == counter and int(r["Grid_Size"]) == grid]
     if not vals:
@@ -45,7 +45,8 @@ def main():
     rd = 2.0 * fetch_kib * 1024.0
     wr = write_kib * 1024.0
     state_bytes = int(lib().f16env_state_bytes_per_env())
-    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes, a.layout) * a.envs
+    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes) * a.envs
+    lay = algorithmic_bytes_per_env_step(a.stack, state_bytes, a.layout) * a.envs  # this layout's own
     d = {
         "kernel": a.kernel, "layout": a.layout, "envs": a.envs, "stack_k": a.stack, "state_bytes": state_bytes,
         "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib, "launches": [nf, nw],
@@ -53,6 +54,8 @@ def main():
         "hbm_bytes_per_launch": int(rd + wr),
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": round((rd + wr) / alg, 4),
+        "layout_bytes_per_launch": lay,
+        "traffic_over_layout_bytes": round((rd + wr) / lay, 4),
         "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes; WRITE_SIZE as read",
     }
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
