@@ -505,6 +505,8 @@ __device__ __forceinline__ void put_slot(float* d, const float* f) {
   st16(q + 3, make_float4(f[12], f[13], f[14], 0.0f));
 }
 static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([4][64] float4)
+static constexpr int WSTASH = 16 * 64;  // ... and for the env-field stash of the 256-register builds
+static constexpr int WIN_WAVE_FLOATS = WFRESH + WSTASH;
 
 template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
@@ -519,6 +521,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
   const int rows = (int)(a.E.n - row0 < 64 ? (a.E.n - row0 > 0 ? a.E.n - row0 : 0) : 64);
   const bool image = a.lds_image != 0;
+#ifdef F16_NO_STASH
+  constexpr bool STASH = false;
+#else
+  constexpr bool STASH = LOWREG && WIN;
+#endif
   float* img = dynl + (size_t)wave * image_floats_per_wave(KC);
   // 1) DMA of this wave's previous stack block into LDS (overlaps the physics)
   auto issue_stack_dma = [&]() {
@@ -565,7 +572,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // (LDS-DMA into the wave's staging area, [15][64] floats, not registers: nothing stays live
   // across the frames; the vmcnt(0) after the frames retires it)
   bool fresh = false;
-  float* stg = dynl + (size_t)wave * WFRESH;
+  float* stg = dynl + (size_t)wave * WIN_WAVE_FLOATS;
   if (live) {
     fresh = (L.flags & LANE_FLAG_FRESH) != 0;
     L.flags &= ~LANE_FLAG_FRESH;
@@ -595,7 +602,34 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     }
     earth_angle(L.epa, ce, se);
     A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
+    // 256-register windowed builds: the env fields the frames never read (goal, last distance,
+    // step, episode count and return) wait in the wave's LDS stash instead of VGPRs, which the
+    // frame loop needs (they were part of what spilled to scratch around it)
+    float4* stash = reinterpret_cast<float4*>(stg + WFRESH);
+    if (STASH) {
+      stash[lane] = make_float4(L.goal[0], L.goal[1], L.goal[2], L.last_d);
+      stash[64 + lane] = make_float4(__int_as_float(L.step), __int_as_float(L.ep_count), dlo(L.ep_ret), dhi(L.ep_ret));
+      // the Earth angle: the frames advance it by a constant each (replayed below, the same
+      // fp64 adds) and otherwise read only its cos / sin; the gust model's pieces: the frames
+      // read the wind sum only
+      stash[128 + lane] = make_float4(dlo(L.epa), dhi(L.epa), GUST ? L.gust[0] : 0.0f, GUST ? L.gust[1] : 0.0f);
+      if (GUST) stash[192 + lane] = make_float4(L.gust[2], L.wst[0], L.wst[1], L.wst[2]);
+      asm volatile("" ::: "memory");
+    }
     for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    if (STASH) {
+      asm volatile("" ::: "memory");
+      const float4 g = stash[lane], e = stash[64 + lane];
+      L.goal[0] = g.x; L.goal[1] = g.y; L.goal[2] = g.z; L.last_d = g.w;
+      L.step = __float_as_int(e.x); L.ep_count = __float_as_int(e.y); L.ep_ret = f2d(e.z, e.w);
+      const float4 w = stash[128 + lane];
+      L.epa = f2d(w.x, w.y);
+      for (int s = 0; s < a.E.down_sample; ++s) L.epa += OMEGA_E * a.C.dt;  // frame()'s per-frame advance
+      if (GUST) {
+        const float4 u = stash[192 + lane];
+        L.gust[0] = w.z; L.gust[1] = w.w; L.gust[2] = u.x; L.wst[0] = u.y; L.wst[1] = u.z; L.wst[2] = u.w;
+      }
+    }
   }
   // Two-waves-per-SIMD builds with no done list to compact (its atomic's return would wait
   // for every store before it): retire the stack DMA and store the state columns the frames
@@ -913,7 +947,7 @@ static StepKernel step_win_kernel_for(int mode, int occ) {
       {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}};
   return table[occ == 2 ? 1 : 0][mode & 3];
 }
-static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WFRESH;
+static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WIN_WAVE_FLOATS;
 // variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
 // roll: the rollout-slot build (f16env_step_rollout); the plain step carries none of its code.
 static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {

@@ -19,6 +19,8 @@ PAT = os.path.join(ROOT, "f16_jsb_amd", "libf16env_var_%s.so")
 CASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4), (65536, 10, 4), (4096, 4, 4)]
 # the same cases in the windowed observation layout (the bench headline's)
 WCASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4), (4096, 4, 4)]
+# cfg5 mode (random ICs + gusts: MODE 3 kernels), window layout
+C5CASES = [(131072, 4, 4), (65536, 4, 4)]
 
 
 def build(specs):
@@ -37,8 +39,10 @@ def run_one():
     import torch
     from f16_jsb_amd.env import F16Envs
     res = {}
-    for lay, n, k, ds in [("c", *c) for c in CASES] + [("w", *c) for c in WCASES]:
-        e = F16Envs(n, stack_k=k, down_sample=ds, seed=1, obs_layout="window" if lay == "w" else "contiguous")
+    runs = [("c", *c) for c in CASES] + [("w", *c) for c in WCASES] + [("w5", *c) for c in C5CASES]
+    for lay, n, k, ds in runs:
+        e = F16Envs(n, stack_k=k, down_sample=ds, seed=1, obs_layout="contiguous" if lay == "c" else "window",
+                    cfg5=lay == "w5")
         e.reset()
         acts = [e.sample_actions(5, t) for t in range(16)]
         for t in range(20):
@@ -50,7 +54,7 @@ def run_one():
             e.step(acts[t % 16])
         en.record()
         torch.cuda.synchronize()
-        res[("w_" if lay == "w" else "") + "n%d_k%d_ds%d" % (n, k, ds)] = round(s.elapsed_time(en) / 300 * 1e3, 2)
+        res[("" if lay == "c" else lay + "_") + "n%d_k%d_ds%d" % (n, k, ds)] = round(s.elapsed_time(en) / 300 * 1e3, 2)
         e.close()
     print(json.dumps(res))
 
