@@ -1083,11 +1083,14 @@ struct ResetDoneArgs {
                     // 16, (p-K+1)*N*16, N*16, 16)
   int64_t obs_row, obs_off, obs_pitch;
   int32_t obs_slot;
+  int32_t* zero_next;  // the handle's other done counter (the next step's): zeroed here, so a
+                       // step needs no memset of its counter
   EnvArgs E;
   ModelConsts C;
 };
 __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) {
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
+  if (a.zero_next && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_next = 0;
   const int nd = *a.n_done;
   if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // block-uniform: no barrier skipped by part of a block
   stage_tables(sT);
@@ -1487,7 +1490,8 @@ struct f16env {
   void* mem;       // state SoA
   void* tmem;      // template SoA (n = 1)
   double* ic_dev;  // default IC, RANDOM_IC box lo, hi (3 x F16_IC_N)
-  int32_t* done_buf;  // deferred modes: own done list (N) + count, when the caller gives none
+  int32_t* done_buf;  // deferred modes: own done list (N) + two counts, when the caller gives none
+  int done_par;       // which of the two counts the next step uses
   unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine counter (device, 8 B) + a
                                   // scratch word (set_state's wind detection)
   int mode;           // step kernel variant: bit 0 RANDOM_IC, bit 1 wind (GUSTS, or lanes with
@@ -1629,11 +1633,13 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   h->done_buf = nullptr;
   if (hipMalloc(&h->tmem, (size_t)TMPL_COLS * 16) != hipSuccess ||
       hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||
-      hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 1)) != hipSuccess) {
+      hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 2)) != hipSuccess) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); delete h;
     return set_err(-3, "hipMalloc(template) failed");
   }
   soa_carve(h->tmem, 1, h->tmpl);
+  hipMemset(h->done_buf + cfg->n_envs, 0, 2 * sizeof(int32_t));
+  h->done_par = 0;
   if (hipMalloc((void**)&h->nonfinite, 2 * sizeof(unsigned long long)) != hipSuccess) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
     return set_err(-3, "hipMalloc(counter) failed");
@@ -1775,6 +1781,25 @@ int f16env_reset(f16env_t h, void* stream, const uint8_t* mask, const float* goa
   return reset_launch(h, (hipStream_t)stream, a);
 }
 
+// The done list of a step: the caller's (its count zeroed here), else, in deferred modes, the
+// handle's own with two alternating counts -- the step's deferred-reset kernel zeroes the one
+// the next step uses, so an auto-resetting step issues no memset (one GPU operation fewer).
+static int done_counter(f16env_t h, int32_t* done_idx, int32_t*& list, int32_t*& count, int32_t*& zero_next,
+                        hipStream_t st) {
+  zero_next = nullptr;
+  if (h->mode && !done_idx) {  // deferred resets need the done list
+    list = h->done_buf;
+    count = h->done_buf + h->cfg.n_envs + h->done_par;
+    if (!(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {  // the reset kernel follows: it zeroes the other
+      zero_next = h->done_buf + h->cfg.n_envs + (h->done_par ^ 1);
+      h->done_par ^= 1;
+      return 0;
+    }
+  }
+  if (count) HIPCHK(hipMemsetAsync(count, 0, sizeof(int32_t), st));
+  return 0;
+}
+
 static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                      const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
                      float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done) {
@@ -1804,11 +1829,8 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   if (((uintptr_t)obs & 15) != 0 || ((uintptr_t)obs_prev & 15) != 0)
     return set_err(-1, "obs and obs_prev must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
-  if (h->mode && !done_idx) {  // deferred resets need the done list
-    a.done_idx = h->done_buf;
-    a.n_done = h->done_buf + h->cfg.n_envs;
-  }
-  if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
+  int32_t* zero_next = nullptr;
+  if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) return e;
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
   const StepKernel kern = step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0), slot != nullptr);
   if (h->prof_next < (int)h->prof_ev.size() / 2) {  // profiling: events from the dispatch packet itself
@@ -1822,6 +1844,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = obs;
     r.obs_row = (int64_t)a.E.K * F16_OBS_DIM; r.obs_off = 0; r.obs_pitch = F16_OBS_DIM; r.obs_slot = F16_OBS_DIM;
+    r.zero_next = zero_next;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
@@ -1888,11 +1911,8 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   a.C = h->C;
   a.lds_image = 0;
   hipStream_t st = (hipStream_t)stream;
-  if (h->mode && !done_idx) {
-    a.done_idx = h->done_buf;
-    a.n_done = h->done_buf + h->cfg.n_envs;
-  }
-  if (a.n_done) HIPCHK(hipMemsetAsync(a.n_done, 0, sizeof(int32_t), st));
+  int32_t* zero_next = nullptr;
+  if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) return e;
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
   const StepKernel kern = step_win_kernel_for(h->mode, h->win_occ);
   if (h->prof_next < (int)h->prof_ev.size() / 2) {
@@ -1906,6 +1926,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
     r.obs_row = Q; r.obs_off = (int64_t)(pos - a.E.K + 1) * P; r.obs_pitch = P; r.obs_slot = WPITCH;
+    r.zero_next = zero_next;
     r.E = a.E; r.C = h->C;
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
