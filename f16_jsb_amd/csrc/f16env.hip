@@ -1015,11 +1015,16 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
 #pragma unroll
       for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = op[j * F16_OBS_DIM + c];
   }
-  float prevf[F16_OBS_DIM];  // newest frame of the observation the next action acts on
-#pragma unroll
-  for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = my[(K - 1) * slot_stride + c];
-  int head = 0;  // ring slot of the oldest frame
+  // head: ring slot of the oldest frame, the same for every lane (a reset rewrites all K slots
+  // and advances it like an append), so the newest frame of the observation an action acts on
+  // -- the rollout slot's frame -- sits in one uniform slot for the whole wave
+  int head = 0;
   const int64_t N = a.E.n;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
+  // a full wave writes its 64 frames (3 840 contiguous bytes) as 240 float4 gathered from the
+  // ring, instead of fifteen 4-byte stores per lane at a 60-byte stride
+  const bool coalesced = a.E.n - row0 >= 64 && (N * F16_OBS_DIM) % 4 == 0 && ((uintptr_t)a.frames & 15) == 0;
   const uint64_t gid = (uint64_t)(a.E.id_base + k);
   for (int t = 0; t < a.T; ++t) {
     const float4 av = philox_action(a.seed, gid, a.step0 + (uint64_t)t);
@@ -1039,9 +1044,26 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
     const int done = fl & 3;
     if (fl & 4) atomicAdd(a.nonfinite, 1ull);  // rare: one lane at a time
     const int64_t row = (int64_t)t * N + k;
-    float* fr = a.frames + row * F16_OBS_DIM;
+    const int nslot = head == 0 ? K - 1 : head - 1;  // newest frame
+    if (coalesced) {
+      __builtin_amdgcn_wave_barrier();
+      const float* src = ring + nslot * slot_stride + (size_t)(wave * 64) * RING_PITCH;
+      float4* dst = reinterpret_cast<float4*>(a.frames + ((int64_t)t * N + row0) * F16_OBS_DIM);
+      for (int q = lane; q < 64 * F16_OBS_DIM / 4; q += 64) {
+        float v[4];
 #pragma unroll
-    for (int c = 0; c < F16_OBS_DIM; ++c) fr[c] = prevf[c];
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * q + i, r = e / F16_OBS_DIM;
+          v[i] = src[r * RING_PITCH + (e - r * F16_OBS_DIM)];
+        }
+        dst[q] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      float* fr = a.frames + row * F16_OBS_DIM;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) fr[c] = my[nslot * slot_stride + c];
+    }
     reinterpret_cast<float4*>(a.actions)[row] = av;
     a.rewards[row] = r32;
     if (t + 1 < a.T) a.next_start[row] = done ? 1.0f : 0.0f;
@@ -1052,16 +1074,11 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
       for (int j = 0; j < K; ++j)
 #pragma unroll
         for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = f0[c];
-      head = 0;
-#pragma unroll
-      for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = f0[c];
     } else {  // deque append (:235): the oldest frame's slot takes the new one
 #pragma unroll
       for (int c = 0; c < F16_OBS_DIM; ++c) my[head * slot_stride + c] = f[c];
-      head = (head + 1 == K) ? 0 : head + 1;
-#pragma unroll
-      for (int c = 0; c < F16_OBS_DIM; ++c) prevf[c] = f[c];
     }
+    head = (head + 1 == K) ? 0 : head + 1;
   }
   lane_store(a.s, k, L);
   float* o = a.obs + k * (int64_t)K * F16_OBS_DIM;

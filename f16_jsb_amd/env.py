@@ -536,14 +536,21 @@ class F16VecEnv(*_bases(SB3VecEnv)):
     packed rewards/flags per step, one stream sync; infos of lanes that did not finish share one
     read-only dict. The obs array returned stays valid for two further steps (see _HostStaging).
     ``return_numpy=False`` keeps everything on the GPU (infos is then None: the caller reads the
-    ``last_step`` device tensors). ``envs=`` wraps an existing handle instead of creating one."""
+    ``last_step`` device tensors). ``envs=`` wraps an existing handle instead of creating one.
+    The handle it creates steps in the windowed observation layout in numpy mode and in the
+    contiguous one in device mode (``obs_layout=`` overrides)."""
 
     metadata = {"render_modes": []}
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
                  return_numpy: bool = True, env_id_base: int = 0, envs=None, **kw):
-        self.envs = envs if envs is not None else F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed,
-                                                          env_id_base=env_id_base, **kw)
+        if envs is None:
+            # numpy mode copies every observation to the host anyway, so the env steps in the
+            # windowed layout (no per-step stack rewrite: 16.9 vs 27.8 us at K = 10, 65 536 envs);
+            # device mode keeps dense (N, K, 15) buffers unless asked otherwise
+            kw.setdefault("obs_layout", "window" if return_numpy else "contiguous")
+            envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, env_id_base=env_id_base, **kw)
+        self.envs = envs
         n = self.envs.n
         self.render_mode = None
         self._attrs: dict = {}
