@@ -691,8 +691,7 @@ __device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRe
 // advanced within the step along the geodetic normal: h = h0 + n . (rE - r0). Over one env
 // step |rE - r0| < 70 ft, so the neglected curvature term |dr|^2/2R < 2e-4 ft (far below the
 // 4e-4 ft fp32 resolution of the observed altitude).
-__device__ __forceinline__ void derive(const Lane& L, double ce, double se, const AltRef& A, Derived& d,
-                                       float* lat_gc_out = nullptr, float* lon_out = nullptr) {
+__device__ __forceinline__ void derive(const Lane& L, double ce, double se, const AltRef& A, Derived& d) {
   const double xE = ce * L.rI[0] + se * L.rI[1];
   const double yE = -se * L.rI[0] + ce * L.rI[1];
   const double zE = L.rI[2];
@@ -714,12 +713,6 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
     const float inv = rcpf(rxyf);
     slon = yi * inv;
     clon = xi * inv;
-  }
-  if (lat_gc_out) {  // geocentric latitude / ECEF longitude for the observation
-    const float xf = (float)xE, yf = (float)yE;
-    const float rxyE = fsqrt(xf * xf + yf * yf);
-    *lat_gc_out = atan2f(zf, rxyE);
-    *lon_out = (rxyE == 0.0f) ? 0.0f : atan2f(yf, xf);
   }
   // Ti2l rows (north, east, down) in ECI
   const float L0 = -clon * slat, L1 = -slon * slat, L2 = clat;
@@ -1083,9 +1076,12 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 // 256-register build takes it)
 // WIND: the lane may carry wind (the wind kernels, IC passes); false skips the air-relative
 // velocity's wind term (reference task: no wind, jsbsim_gym.py never enables FGWinds).
-template <bool LOWREG = false, bool WIND = true>
+// KEEP: `keep` receives this frame's Derived (the last frame's is what the observation frame
+// of the step needs: accelerations do not move the state make_frame derives from).
+template <bool LOWREG = false, bool WIND = true, bool KEEP = false>
 __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se, const AltRef& A,
-                                      const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
+                                      const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG,
+                                      Derived* keep = nullptr) {
   const float dt = (float)C.dt;
   const FcsTab tb = fcs_tables(L, T);
   if (!ic) {
@@ -1131,6 +1127,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F16_STAMP(stamps, ST_PROP);
   Derived d;
   derive(L, ce, se, A, d);
+  if (KEEP) *keep = d;
   F16_STAMP(stamps, ST_DERIVE);
   // -- Auxiliary, wind-axis part (needs no atmosphere) --
   float wb[3] = {0.0f, 0.0f, 0.0f};

@@ -240,10 +240,16 @@ __device__ __forceinline__ float norm_angle(float a) {
   return (float)x;
 }
 // _get_current_single_observation (jsbsim_gym.py:172-197)
-__device__ void make_frame(const Lane& L, double ce, double se, const AltRef& A, float* f) {
-  Derived d;
-  float lat, lon;
-  derive(L, ce, se, A, d, &lat, &lon);
+// make_frame from the last FDM frame's Derived (the same inputs: a frame's accelerations do
+// not move rI, vI, q, wI, so its derive() equals make_frame's), bit-identical; only the
+// latitude / longitude are evaluated here.
+__device__ void make_frame_from(const Lane& L, double ce, double se, const Derived& d, float* f) {
+  const double xE = ce * L.rI[0] + se * L.rI[1];
+  const double yE = -se * L.rI[0] + ce * L.rI[1];
+  const float xf = (float)xE, yf = (float)yE, zf = (float)L.rI[2];
+  const float rxyE = fsqrt(xf * xf + yf * yf);
+  const float lat = atan2f(zf, rxyE);
+  const float lon = (rxyE == 0.0f) ? 0.0f : atan2f(yf, xf);
   float phi, tht, psi;
   euler(d.Tl2b, phi, tht, psi);
   f[0] = (float)((double)lat * 6.3781e6);
@@ -255,6 +261,11 @@ __device__ void make_frame(const Lane& L, double ce, double se, const AltRef& A,
   f[6] = d.pqr[0]; f[7] = d.pqr[1]; f[8] = d.pqr[2];
   f[9] = norm_angle(phi); f[10] = norm_angle(tht); f[11] = norm_angle(psi);
   f[12] = L.goal[0]; f[13] = L.goal[1]; f[14] = L.goal[2];
+}
+__device__ void make_frame(const Lane& L, double ce, double se, const AltRef& A, float* f) {
+  Derived d;
+  derive(L, ce, se, A, d);
+  make_frame_from(L, ce, se, d, f);
 }
 __device__ __forceinline__ float norm3f(float a, float b, float c) {
 #pragma clang fp contract(off)
@@ -588,6 +599,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   int flags_out = 0;
   double ce = 1.0, se = 0.0;
   AltRef A;
+  Derived d_last;  // the last frame's, for the observation frame (one-wave builds)
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
@@ -616,7 +628,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (GUST) stash[192 + lane] = make_float4(L.gust[2], L.wst[0], L.wst[1], L.wst[2]);
       asm volatile("" ::: "memory");
     }
-    for (int s = 0; s < a.E.down_sample; ++s) frame<LOWREG, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    for (int s = 0; s < a.E.down_sample; ++s)  // :225-232
+      frame<LOWREG, GUST, !LOWREG>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS, &d_last);
     if (STASH) {
       asm volatile("" ::: "memory");
       const float4 g = stash[lane], e = stash[64 + lane];
@@ -643,7 +656,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     if (live) lane_store<GUST, 1>(a.s, k, L);
   }
   if (live) {
-    make_frame(L, ce, se, A, f);                              // :234
+    if (!LOWREG && a.E.down_sample > 0) make_frame_from(L, ce, se, d_last, f);  // :234
+    else make_frame(L, ce, se, A, f);
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261), PositionReward (:493-507)
     float r32;
