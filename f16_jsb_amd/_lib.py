@@ -60,6 +60,9 @@ def lib():
     _set(L, "f16env_step_mode", [vp], i32)
     _set(L, "f16env_features_strided", [vp, i64, i32, vp, i64, i64, vp], i32)
     _set(L, "f16env_set_window_order", [vp, i32], i32)
+    _set(L, "f16env_window_bind", [vp, vp, vp, i64, vp, vp, vp, vp, vp], i32)
+    _set(L, "f16env_window_step_bound", [vp, vp, vp, i32, i32], i32)
+    _set(L, "f16env_step_window_nt", [vp], i32)
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_nonfinite_count.argtypes = [vp, vp, ctypes.POINTER(u64)]
     L.f16env_rollout_random.argtypes = [vp, vp, u64, u64, i32] + [vp] * 7
@@ -100,6 +103,7 @@ EXPORTED_SYMBOLS = (
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
     "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order",
+    "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt",
     "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",

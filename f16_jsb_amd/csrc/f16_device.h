@@ -238,10 +238,22 @@ __device__ __forceinline__ void latch_from_state(Lane& L) {
                                    (float)L.rI[0], (float)L.rI[1], (float)L.rI[2]);
 }
 
-// 16-B output store of the step kernels (state columns, history frame slots): plain
-// global_store_dwordx4. Write-through (buffer store sc1) and non-temporal forms were measured
-// slower, the window layout's 64-B slot writes up to 2x (profiles/r02_variants_store.json).
-__device__ __forceinline__ void st16(float4* p, float4 v) { *p = v; }
+// 16-B output store of the step kernels (state columns, window frame slots); NT: non-temporal
+// (global_store_dwordx4 ... nt; a compile-time choice: as a runtime branch the compiler merges
+// the two stores and drops the hint), which the windowed step uses when its whole grid is
+// resident at once (f16_step_win_nt_kernel: 65 536 envs 17.2-17.6 -> 16.6-16.7 us, 131 072 25.0 -> 23.5,
+// cfg5 131 072 34.7 -> 32.6; 262 144 envs, two rounds of waves, 47.1 -> 49.3, so not there;
+// the contiguous layout is slower with it everywhere; write-through sc1 slower everywhere:
+// profiles/r02_variants_store*.json, r02_variants_nt*.json)
+template <bool NT = false>
+__device__ __forceinline__ void st16(float4* p, float4 v) {
+  if (NT) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(__builtin_bit_cast(v4f, v), reinterpret_cast<v4f*>(p));
+  } else {
+    *p = v;
+  }
+}
 
 template <bool GUST>
 __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, float4 g, Lane& L) {
@@ -300,7 +312,7 @@ __device__ __forceinline__ void lane_load_lds(const float4* cols, Lane& L) {
 
 // PART: 0 every column; 1 the columns a step's frames leave final (all but C3 and C15, which
 // the env layer still changes: episode return, last distance, and a reset); 2 C3 and C15.
-template <bool GUST = false, int PART = 0>
+template <bool GUST = false, int PART = 0, bool NT = false>
 __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
   const int64_t n = s.n;
   float4 c[NCOL];
@@ -324,10 +336,10 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n)
-    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) st16(p, c[j]);
+    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) st16<NT>(p, c[j]);
   if (GUST && PART != 2) {
-    st16(p, make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f));
-    st16(p + n, make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f));
+    st16<NT>(p, make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f));
+    st16<NT>(p + n, make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f));
   }
 }
 
@@ -1076,12 +1088,9 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 // 256-register build takes it)
 // WIND: the lane may carry wind (the wind kernels, IC passes); false skips the air-relative
 // velocity's wind term (reference task: no wind, jsbsim_gym.py never enables FGWinds).
-// KEEP: `keep` receives this frame's Derived (the last frame's is what the observation frame
-// of the step needs: accelerations do not move the state make_frame derives from).
-template <bool LOWREG = false, bool WIND = true, bool KEEP = false>
+template <bool LOWREG = false, bool WIND = true>
 __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se, const AltRef& A,
-                                      const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG,
-                                      Derived* keep = nullptr) {
+                                      const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
   const float dt = (float)C.dt;
   const FcsTab tb = fcs_tables(L, T);
   if (!ic) {
@@ -1127,7 +1136,6 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F16_STAMP(stamps, ST_PROP);
   Derived d;
   derive(L, ce, se, A, d);
-  if (KEEP) *keep = d;
   F16_STAMP(stamps, ST_DERIVE);
   // -- Auxiliary, wind-axis part (needs no atmosphere) --
   float wb[3] = {0.0f, 0.0f, 0.0f};

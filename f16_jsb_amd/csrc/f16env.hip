@@ -240,9 +240,12 @@ __device__ __forceinline__ float norm_angle(float a) {
   return (float)x;
 }
 // _get_current_single_observation (jsbsim_gym.py:172-197)
-// make_frame from the last FDM frame's Derived (the same inputs: a frame's accelerations do
-// not move rI, vI, q, wI, so its derive() equals make_frame's), bit-identical; only the
-// latitude / longitude are evaluated here.
+// The observation frame (jsbsim_gym.py:172-197) from the derived quantities of the lane's
+// state; the latitude / longitude are evaluated here. (Reusing the last FDM frame's Derived
+// instead -- the frame's accelerations do not move rI, vI, q, wI -- saved 0.7 us per step at
+// 4 096 envs and nothing at 65 536 in the windowed step, r02_variants_keep.json, but the
+// two builds then round the observation differently: kept out, the one- and two-waves-per-
+// SIMD builds stay bit-identical.)
 __device__ void make_frame_from(const Lane& L, double ce, double se, const Derived& d, float* f) {
   const double xE = ce * L.rI[0] + se * L.rI[1];
   const double yE = -se * L.rI[0] + ce * L.rI[1];
@@ -508,18 +511,19 @@ __device__ __forceinline__ size_t image_floats_per_wave(int KC) { return (size_t
 // (no copy). The other parity's window is untouched by a step, so an observation stays valid
 // until the step after next, as with the ping-pong buffers of f16env_step.
 static constexpr int WPITCH = 16;  // floats per history frame slot
+template <bool NT = false>
 __device__ __forceinline__ void put_slot(float* d, const float* f) {
   float4* q = reinterpret_cast<float4*>(d);
-  st16(q, make_float4(f[0], f[1], f[2], f[3]));
-  st16(q + 1, make_float4(f[4], f[5], f[6], f[7]));
-  st16(q + 2, make_float4(f[8], f[9], f[10], f[11]));
-  st16(q + 3, make_float4(f[12], f[13], f[14], 0.0f));
+  st16<NT>(q, make_float4(f[0], f[1], f[2], f[3]));
+  st16<NT>(q + 1, make_float4(f[4], f[5], f[6], f[7]));
+  st16<NT>(q + 2, make_float4(f[8], f[9], f[10], f[11]));
+  st16<NT>(q + 3, make_float4(f[12], f[13], f[14], 0.0f));
 }
 static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-frame DMA ([4][64] float4)
 static constexpr int WSTASH = 16 * 64;  // ... and for the env-field stash of the 256-register builds
 static constexpr int WIN_WAVE_FLOATS = WFRESH + WSTASH;
 
-template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false>
+template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
@@ -599,7 +603,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   int flags_out = 0;
   double ce = 1.0, se = 0.0;
   AltRef A;
-  Derived d_last;  // the last frame's, for the observation frame (one-wave builds)
   if (live) {
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;                                              // jsbsim_gym.py:215
@@ -629,7 +632,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       asm volatile("" ::: "memory");
     }
     for (int s = 0; s < a.E.down_sample; ++s)  // :225-232
-      frame<LOWREG, GUST, !LOWREG>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS, &d_last);
+      frame<LOWREG, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);
     if (STASH) {
       asm volatile("" ::: "memory");
       const float4 g = stash[lane], e = stash[64 + lane];
@@ -653,11 +656,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   const bool early_store = LOWREG && !a.done_idx;
   if (early_store) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (live) lane_store<GUST, 1>(a.s, k, L);
+    if (live) lane_store<GUST, 1, NT>(a.s, k, L);
   }
   if (live) {
-    if (!LOWREG && a.E.down_sample > 0) make_frame_from(L, ce, se, d_last, f);  // :234
-    else make_frame(L, ce, se, A, f);
+    make_frame(L, ce, se, A, f);  // :234
     F16_STAMP(stamps, ST_FRAME_OBS);
     // reward / termination (:237-261), PositionReward (:493-507)
     float r32;
@@ -707,9 +709,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     F16_STAMP(stamps, ST_RESET);
 #ifndef F16_DIAG_SKIP_STORE
     if (!early_store || (done && !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
-      lane_store<GUST>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
+      lane_store<GUST, 0, NT>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
     else
-      lane_store<GUST, 2>(a.s, k, L);  // the rest
+      lane_store<GUST, 2, NT>(a.s, k, L);  // the rest
 #else
     if (L.step == -12345) lane_store<GUST>(a.s, k, L);
 #endif
@@ -791,14 +793,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 16 * j + (lane >> 2);
-          st16(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wenv), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
+          st16<NT>(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wenv), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
         }
       }
       __builtin_amdgcn_wave_barrier();
     } else if (live) {
       const int64_t off = k * a.wenv + (int64_t)p * a.wrow;
-      put_slot(a.wx + off, reset_now ? f0 : f);
-      put_slot(a.wy + off, f);
+      put_slot<NT>(a.wx + off, reset_now ? f0 : f);
+      put_slot<NT>(a.wy + off, f);
     }
     F16_STAMP(stamps, ST_COPY);
   } else if (kSkipStack) {
@@ -954,12 +956,22 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_kernel(StepArgs a) {
   STEP_SHARED
   step_body<MODE, false, false, OCC == 2, true>(a, sT, sTmpl, sDone, dynl);
 }
+// ... with non-temporal state and frame-slot stores, for grids resident in one round (st16)
+template <int MODE, int OCC>
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(StepArgs a) {
+  STEP_SHARED
+  step_body<MODE, false, false, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl);
+}
 using StepKernel = void (*)(StepArgs);
-static StepKernel step_win_kernel_for(int mode, int occ) {
-  static const StepKernel table[2][4] = {
-      {f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
-      {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}};
-  return table[occ == 2 ? 1 : 0][mode & 3];
+static StepKernel step_win_kernel_for(int mode, int occ, int nt) {
+  static const StepKernel table[2][2][4] = {
+      {{f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
+       {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}},
+      {{f16_step_win_nt_kernel<0, 1>, f16_step_win_nt_kernel<1, 1>, f16_step_win_nt_kernel<2, 1>,
+        f16_step_win_nt_kernel<3, 1>},
+       {f16_step_win_nt_kernel<0, 2>, f16_step_win_nt_kernel<1, 2>, f16_step_win_nt_kernel<2, 2>,
+        f16_step_win_nt_kernel<3, 2>}}};
+  return table[nt ? 1 : 0][occ == 2 ? 1 : 0][mode & 3];
 }
 static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WIN_WAVE_FLOATS;
 // variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
@@ -1530,6 +1542,15 @@ struct f16env {
   int occ;            // waves per SIMD the step kernel is compiled for (1 or 2)
   int win_occ;        // the same for the windowed-observation step kernel
   int win_env_major;  // window histories [N][T][16] (1) instead of the default [T][N][16] (0)
+  int win_nt;         // windowed step: non-temporal output stores
+  struct {            // f16env_window_bind: the buffers of f16env_window_step_bound
+    float* hist[2];
+    int64_t T;
+    float* rew;
+    uint8_t *term, *trunc;
+    double* ep_ret;
+    int32_t* ep_len;
+  } wb;
   SoA soa, tmpl;
   ModelConsts C;
   size_t bytes;
@@ -1698,6 +1719,10 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     if (getenv("F16ENV_OCC")) h->occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
     h->win_occ = (waves > 4 * (int64_t)cus && 2 * (static_lds + WIN_DYN_LDS) <= 160 * 1024) ? 2 : 1;
     if (getenv("F16ENV_OCC")) h->win_occ = atoi(getenv("F16ENV_OCC")) == 2 ? 2 : 1;
+    // non-temporal output stores pay in the windowed step when its whole grid is resident at
+    // once (one round of waves); with more rounds they cost (st16)
+    h->win_nt = waves <= (int64_t)h->win_occ * 4 * cus ? 1 : 0;
+    if (getenv("F16ENV_WIN_NT")) h->win_nt = atoi(getenv("F16ENV_WIN_NT")) ? 1 : 0;
     for (int v = 0; v <= 2; ++v) {
       const size_t st_v = v == 2 ? static_gt : static_lds;
       for (int m = 0; m < 8; ++m) {
@@ -1945,7 +1970,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   int32_t* zero_next = nullptr;
   if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) return e;
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  const StepKernel kern = step_win_kernel_for(h->mode, h->win_occ);
+  const StepKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt);
   if (h->prof_next < (int)h->prof_ev.size() / 2) {
     const int i = h->prof_next++;
     hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)WIN_DYN_LDS, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u, a);
@@ -1964,6 +1989,26 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
     HIPCHK(hipGetLastError());
   }
   return 0;
+}
+
+int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float* rew, uint8_t* terminated,
+                       uint8_t* truncated, double* ep_return, int32_t* ep_len) {
+  if (!h) return set_err(-1, "null handle");
+  if (!hist0 || !hist1 || hist0 == hist1 || !rew || !terminated || !truncated)
+    return set_err(-1, "two distinct histories and rew/terminated/truncated are required");
+  if (int e = window_check(h, hist0, hist1, T, h->cfg.stack_k - 1)) return e;
+  h->wb.hist[0] = hist0; h->wb.hist[1] = hist1; h->wb.T = T;
+  h->wb.rew = rew; h->wb.term = terminated; h->wb.trunc = truncated;
+  h->wb.ep_ret = ep_return; h->wb.ep_len = ep_len;
+  return 0;
+}
+
+int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos) {
+  if (!h) return set_err(-1, "null handle");
+  if (!h->wb.hist[0]) return set_err(-1, "f16env_window_bind first");
+  const int b = parity & 1;
+  return f16env_step_window(h, stream, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew, h->wb.term,
+                            h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr);
 }
 
 int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
@@ -1998,6 +2043,7 @@ int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, 
 }
 
 int f16env_step_window_waves_per_simd(f16env_t h) { return h ? h->win_occ : 0; }
+int f16env_step_window_nt(f16env_t h) { return h ? h->win_nt : -1; }
 
 int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                         const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,

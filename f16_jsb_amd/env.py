@@ -126,6 +126,9 @@ class F16Envs:
             self._win_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
                              self.ep_return.data_ptr(), self.ep_len.data_ptr())
             self._step_win_fn = L.f16env_step_window
+            check(L.f16env_window_bind(self._h, self._hist_ptr[0], self._hist_ptr[1], self.T, *self._win_ptr),
+                  "f16env_window_bind")
+            self._step_bound = L.f16env_window_step_bound
             self.terminal_obs = self._window(1)
         else:
             self._obs_ptr = [o.data_ptr() for o in self._obs]
@@ -184,7 +187,8 @@ class F16Envs:
     def step_kernel_name(self) -> str:
         mode = int(lib().f16env_step_mode(self._h))
         if self.window:
-            return "f16_step_win_kernel<%d, %d>" % (mode, self.waves_per_simd)
+            nt = int(lib().f16env_step_window_nt(self._h)) == 1
+            return "f16_step_win%s_kernel<%d, %d>" % ("_nt" if nt else "", mode, self.waves_per_simd)
         variant = int(lib().f16env_step_variant(self._h))
         if variant == 2:
             return "f16_step_gt_kernel<%d>" % mode
@@ -301,8 +305,11 @@ class F16Envs:
                   "f16env_window_restart")
             p = self.k - 1
         cur = self._cur ^ 1
-        check(self._step_win_fn(self._h, s, act.data_ptr(), self._hist_ptr[cur], self._hist_ptr[cur ^ 1], self.T, p,
-                                *self._win_ptr, _ptr(done_idx), _ptr(n_done)), "f16env_step_window")
+        if done_idx is None:  # the common case: five arguments, the rest bound at creation
+            check(self._step_bound(self._h, s, act.data_ptr(), cur, p), "f16env_window_step_bound")
+        else:
+            check(self._step_win_fn(self._h, s, act.data_ptr(), self._hist_ptr[cur], self._hist_ptr[cur ^ 1], self.T,
+                                    p, *self._win_ptr, _ptr(done_idx), _ptr(n_done)), "f16env_step_window")
         self._cur, self._p = cur, p
         self.terminal_obs = self._window(1)
         return StepOut(self._window(), self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return,
@@ -729,7 +736,10 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
                  return_numpy: bool = True, envs=None, **kw):
-        self.envs = envs if envs is not None else F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
+        if envs is None:  # as F16VecEnv: the windowed layout when observations go to the host
+            kw.setdefault("obs_layout", "window" if return_numpy else "contiguous")
+            envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
+        self.envs = envs
         self.num_envs = self.envs.n
         self.single_observation_space = spaces.observation_space(self.envs.k)
         self.single_action_space = spaces.action_space()

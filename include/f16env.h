@@ -223,6 +223,12 @@ int f16env_step(f16env_t h, void* stream, const float* act, const float* obs_pre
 int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_cur, float* hist_other,
                        int64_t T, int32_t pos, float* rew, uint8_t* terminated, uint8_t* truncated,
                        double* ep_return, int32_t* ep_len, int32_t* done_idx, int32_t* n_done);
+/* f16env_step_window with the handle's buffers bound once (a per-step call of five arguments:
+ * the host cost of a step is the launch, not the argument marshalling). hist_cur = hist[parity],
+ * hist_other = hist[parity ^ 1]; the pointers must stay valid while bound. */
+int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float* rew, uint8_t* terminated,
+                       uint8_t* truncated, double* ep_return, int32_t* ep_len);
+int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos);
 /* f16env_reset for windowed observations: K copies of frame 0 into hist_cur's window ending at
  * pos (mask / goals / ic as f16env_reset; jsbsim_gym.py:289-331 x N). */
 int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
@@ -233,8 +239,10 @@ int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, 
  * above; 1 env-major N x T x 16 (view strides T*16, 16, 1). Set before the first windowed call
  * and keep it: the histories must be laid out accordingly. */
 int f16env_set_window_order(f16env_t h, int env_major);
-/* Waves per SIMD the windowed step kernel of this handle is built for (1 or 2). */
+/* Waves per SIMD the windowed step kernel of this handle is built for (1 or 2), and whether it
+ * is the non-temporal-store build (1: the whole grid resident in one round of waves). */
 int f16env_step_window_waves_per_simd(f16env_t h);
+int f16env_step_window_nt(f16env_t h);
 
 /* One env step that also fills one slot of a device rollout buffer (SURVEY.md 8f rank 1,
  * replacing the per-step stable_baselines3 RolloutBuffer.add, buffers.py:440-479, and the

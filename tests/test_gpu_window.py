@@ -81,7 +81,7 @@ def test_window_matches_contiguous(gpu, k, T, n, max_steps):
 def test_window_headline_size(gpu):
     """BASELINE cfg3 size (65 536 envs, K = 4): the one-wave window kernel over a restart."""
     a, b = _pair(65536, 4, 16, max_steps=1200)
-    assert b.step_kernel_name == "f16_step_win_kernel<0, 1>"
+    assert b.step_kernel_name == "f16_step_win_nt_kernel<0, 1>"
     _run(a, b, 20, validity=False)
 
 
@@ -96,7 +96,7 @@ def test_window_two_waves_per_simd(gpu, monkeypatch):
 def test_window_cfg5_deferred_resets(gpu):
     """cfg5 modes: random IC + gusts, resets by f16_reset_done_kernel into the window."""
     a, b = _pair(512, 4, 8, max_steps=5, cfg5=True)
-    assert b.step_kernel_name == "f16_step_win_kernel<3, 1>"
+    assert b.step_kernel_name == "f16_step_win_nt_kernel<3, 1>"
     assert _run(a, b, 30) > 512
 
 
@@ -112,7 +112,9 @@ def test_window_caller_resets(gpu):
         done = (sa.terminated | sa.truncated).to(torch.uint8)
         if t % 3 == 0:
             ra, rb = a.reset(mask=done), b.reset(mask=done)
-            np.testing.assert_array_equal(_np(rb), _np(ra))
+            m = _np(done).astype(bool)  # the reset rows come from the same reset kernel: bit-exact
+            np.testing.assert_array_equal(_np(rb)[m], _np(ra)[m])
+            _close(_np(rb)[~m], _np(ra)[~m], "unreset rows @%d" % t)
 
 
 def test_window_set_state_and_obs(gpu):
