@@ -78,6 +78,7 @@ __device__ __forceinline__ void rng_goal(uint64_t seed, uint64_t gid, uint32_t e
 // cfg5 random IC (include/f16env.h F16_FLAG_RANDOM_IC), mirrors oracle rng_ic()
 __device__ void rng_ic(uint64_t seed, uint64_t gid, uint32_t ep, const double* lo, const double* hi, double* ic) {
   uint32_t o[4];
+#pragma unroll  // constant indices: ic[] and o[] stay in registers (no scratch)
   for (int j = 0; j < F16_IC_N; ++j) {
     if ((j & 3) == 0)
       philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), ep,
@@ -150,9 +151,12 @@ __device__ __forceinline__ void frame_features(const float* o, float* y) {
 // ------------------------------------------------------------------------------------------
 __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelConsts& C) {
   const double lat = ic[F16_IC_LAT_GEOD_RAD], lon = ic[F16_IC_LON_RAD], h = ic[F16_IC_H_SL_FT];
-  const double sl = sin(lat), cl = cos(lat);
+  // (sincos: one argument reduction per angle, the same values as sin / cos)
+  double sl, cl, slo, clo;
+  sincos(lat, &sl, &cl);
+  sincos(lon, &slo, &clo);
   const double N = WGS_A / sqrt(1.0 - E2 * sl * sl);
-  const double rE[3] = {(N + h) * cl * cos(lon), (N + h) * cl * sin(lon), (EC2 * N + h) * sl};
+  const double rE[3] = {(N + h) * cl * clo, (N + h) * cl * slo, (EC2 * N + h) * sl};
   L.epa = 0.0;
   for (int j = 0; j < 3; ++j) L.rI[j] = rE[j];
   const double rxy = sqrt(rE[0] * rE[0] + rE[1] * rE[1]);
@@ -161,7 +165,10 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   const double slon = rxy == 0.0 ? 0.0 : rE[1] / rxy, clon = rxy == 0.0 ? 1.0 : rE[0] / rxy;
   const double Lm[9] = {-clon * slat, -slon * slat, clat, -slon, clon, 0.0, -clon * clat, -slon * clat, -slat};
   const double ph = ic[F16_IC_PHI_RAD], th = ic[F16_IC_THETA_RAD], ps = ic[F16_IC_PSI_RAD];
-  const double cp = cos(ph), sp = sin(ph), ct = cos(th), st = sin(th), cs = cos(ps), ss = sin(ps);
+  double cp, sp, ct, st, cs, ss;
+  sincos(ph, &sp, &cp);
+  sincos(th, &st, &ct);
+  sincos(ps, &ss, &cs);
   const double Tl[9] = {ct * cs, ct * ss, -st,
                         sp * st * cs - cp * ss, sp * st * ss + cp * cs, sp * ct,
                         cp * st * cs + sp * ss, cp * st * ss - sp * cs, cp * ct};
