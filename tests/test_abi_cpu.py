@@ -85,6 +85,26 @@ def test_create_without_gpu_fails_loudly(so_path):
         F16Envs(4)
 
 
+def test_null_handle_calls_return_errors(so_path):
+    """Every handle-taking entry point of the windowed / features ABI refuses a NULL handle or
+    a bad argument with a negative status and a message (no device needed, nothing launched)."""
+    from f16_jsb_amd import _lib
+    L = _lib.lib()
+    assert L.f16env_set_window_order(None, 1) < 0
+    assert L.f16env_window_bind(None, None, None, 8, None, None, None, None, None) < 0
+    assert L.f16env_window_step_bound(None, None, None, 0, 3) < 0
+    assert L.f16env_step_window_nt(None) == -1
+    assert L.f16env_step_window_waves_per_simd(None) == 0
+    assert L.f16env_step_window(None, None, None, None, None, 8, 3, None, None, None, None, None, None, None) < 0
+    assert L.f16env_window_restart(None, None, None, None, 8, 7) < 0
+    assert L.f16env_reset_window(None, None, None, None, None, None, 8, 3) < 0
+    # features on a strided block: bad shapes / strides are refused before any launch
+    assert L.f16env_features_strided(None, 4, 0, None, 16, 16, None) < 0
+    assert L.f16env_features_strided(None, 4, 2, None, -1, 16, None) < 0
+    assert L.f16env_features_strided(None, 0, 2, None, 16, 16, None) == 0  # empty: nothing to do
+    assert L.f16env_last_error()
+
+
 def test_product_never_imports_oracle(so_path):
     """No code path of the product reaches the oracle: no Python import of it, no #include
     of oracle/ sources, and libf16env.so does not link it."""
