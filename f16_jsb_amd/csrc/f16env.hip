@@ -1202,9 +1202,15 @@ __global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wenv, in
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * per) return;
   const int64_t b = i >= per, t = i - b * per;
+  float* h = b ? h1 : h0;
+  if (wenv == 4 * 4 && wpos == n * 16) {  // position-major: the K-1 positions are one block
+    float4* h4 = reinterpret_cast<float4*>(h);
+    h4[t] = h4[(int64_t)p_src * n * 4 + t];
+    return;
+  }
   const int64_t q = t & 3, u = t >> 2;
-  const int64_t k = u % n, r = u / n;  // position-major order: consecutive lanes, consecutive envs
-  float* d = (b ? h1 : h0) + k * wenv + r * wpos + 4 * q;
+  const int64_t k = u % n, r = u / n;
+  float* d = h + k * wenv + r * wpos + 4 * q;
   *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(d + (int64_t)p_src * wpos);
 }
 

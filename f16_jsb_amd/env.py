@@ -46,8 +46,9 @@ def _ptr(t) -> Optional[int]:
 
 
 def _default_history(k: int) -> int:
-    """Default window history T (positions per history): max(128, 2K)."""
-    return max(128, 2 * k)
+    """Default window history T (positions per history): max(256, 2K) -- a restart (K-1
+    positions moved to the front) every T-K+1 steps; 2 x 256 x 64 B = 32 KiB per env."""
+    return max(256, 2 * k)
 
 
 class F16Envs:
@@ -61,7 +62,7 @@ class F16Envs:
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
         `history` positions of 64-B frame slots, position-major [T][N][16] (f16env_step_window:
         only the new frame is written per step, one contiguous block per position; view strides
-        (16, N*16, 1)); history 0 = max(128, 2K) (a restart every T-K+1 steps); window_order
+        (16, N*16, 1)); history 0 = max(256, 2K) (a restart every T-K+1 steps); window_order
         "env" keeps the histories env-major [N][T][16] instead (strides (T*16, 16, 1)). Both
         layouts give identical values and the same validity (an observation stays valid until
         the step after next). A consumer that needs a flat (N, K*15) array copies the window

@@ -144,7 +144,7 @@ def test_default_history():
     from f16_jsb_amd.env import _default_history
     for k in (1, 4, 10, 63, 100, 200):
         T = _default_history(k)
-        assert T >= 2 * k and T >= 128
+        assert T >= 2 * k and T >= 256
 
 
 def test_features_rejects_bad_input():
