@@ -460,9 +460,6 @@ struct Atm {
   float T, P, rho, a;
 };
 __device__ __forceinline__ Atm atmosphere(float h_ft) {
-#ifdef F16_DIAG_NO_ATM  // timing ablation only (wrong results): constant 5000 ft atmosphere
-  return Atm{500.9f, 1761.0f, 0.002048f, 1097.0f};
-#endif
   // layer bases (geopotential m), lapse (K/m), base T (K), base P (Pa) -- same recurrence
   // as the oracle, evaluated at compile time below
   constexpr float Hb[8] = {0.0f, 11000.0f, 20000.0f, 32000.0f, 47000.0f, 51000.0f, 71000.0f, 84852.0f};
@@ -859,13 +856,6 @@ __device__ __forceinline__ FcsTab fcs_tables(const Lane& L, const float* T) {
 __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33, float v_fps,
                                         const float* T, const FcsTab& tb, const ModelConsts& C, float dt, bool ic,
                                         FcsOut& o) {
-#ifdef F16_DIAG_NO_FCS  // timing ablation only: surfaces follow the commands directly
-  if (!ic) {
-    o.de = cmd[1] * 0.436f; o.da = cmd[0] * 0.375f; o.dr = cmd[2] * 0.524f; o.dlef = 0.0f; o.flap_mix = 0.0f;
-    o.dsb = 0.0f; o.throttle = cmd[3] * 2.0f;
-    return;
-  }
-#endif
   // qc: the impact-pressure latch (vcas_from_qc); "vc < V kts" is "qc < qc(V)"
   const float alpha = L.lx[F16L_ALPHA], mach = L.lx[F16L_MACH], qc = L.lx[F16L_VC_KTS];
   // Flaps
@@ -918,9 +908,6 @@ __device__ __forceinline__ float seekf(float v, float target, float accel, float
 }
 __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float mach, float h_rho,
                                             float sigma, const float* T, float dt, bool ic) {
-#ifdef F16_DIAG_NO_ENGINE  // timing ablation only
-  if (!ic) return 10000.0f * throttle_pos;
-#endif
   float tp = throttle_pos, aug_cmd = 0.0f;
   if (tp > 1.0f) { aug_cmd = tp - 1.0f; tp -= aug_cmd; }
   // IdleThrust / MilThrust / AugThrust on one (mach 0..2.6 step 0.2) x (density-alt
@@ -970,14 +957,6 @@ struct AeroIn {
   float de, da, dr, dlef, flap, dsb;
 };
 __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6) {
-#ifdef F16_DIAG_NO_AERO  // timing ablation only: linear stand-in, no table lookups
-  {
-    const float qS = a.qbar * S_W;
-    F6[0] = qS * (0.02f + 0.1f * a.alpha); F6[1] = qS * -0.5f * a.beta; F6[2] = qS * (0.1f + 4.0f * a.alpha);
-    F6[3] = qS * -0.01f * a.p; F6[4] = qS * (-0.5f * a.alpha - 0.3f * a.de); F6[5] = qS * 0.05f * a.beta;
-    return;
-  }
-#endif
   const Seg sa = bracket(BP_alpha_bp, T + OFF_pair_alpha, a.alpha);
   // 16 alpha 1-D tables, [12][16 values | 16 alpha-slopes]; FGTable 1-D semantics (clamp
   // at the ends)

@@ -562,9 +562,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + IMG_OFF + 4 * n16);  // tail, never past the end
     }
   };
-#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && defined(F16_DMA_FIRST)
-  issue_stack_dma();
-#endif
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = k < a.E.n;
   int done = 0;
@@ -585,9 +582,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-#if !defined(F16_DIAG_SKIP_STACK) && !defined(F16_DIAG_SKIP_DMA) && !defined(F16_DMA_FIRST)
   issue_stack_dma();
-#endif
   if (ROLL && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
   // a lane reset since the last step: the windowed step reads its reset frame (wy[p-1]) now,
   // so the load streams in behind the physics
@@ -714,25 +709,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       }
     }
     F16_STAMP(stamps, ST_RESET);
-#ifndef F16_DIAG_SKIP_STORE
     if (!early_store || (done && !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
       lane_store<GUST, 0, NT>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
     else
       lane_store<GUST, 2, NT>(a.s, k, L);  // the rest
-#else
-    if (L.step == -12345) lane_store<GUST>(a.s, k, L);
-#endif
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
   // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel
   const bool autoreset = !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET);
-  // F16_DIAG_SKIP_* : timing experiments only (results are wrong with them)
-#ifdef F16_DIAG_SKIP_STACK
-  constexpr bool kSkipStack = true;
-#else
-  constexpr bool kSkipStack = false;
-#endif
   // rollout slot frame = newest frame of obs_prev (what the policy acted on), for every lane
   if (ROLL && a.r_frame && rows > 0) {
     if (image) {
@@ -810,7 +795,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       put_slot<NT>(a.wy + off, f);
     }
     F16_STAMP(stamps, ST_COPY);
-  } else if (kSkipStack) {
   } else if (image) {
     // 2) splice the new frame of row r into the image at row r+1's first frame, which the
     //    shifted copy never reads: out_flat[j] = img[j + 15] for the whole block. The stack
@@ -847,7 +831,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       float* out = a.obs + row0 * KC;
       const int total = rows * KC, n4 = total >> 2;
       float4* out4 = reinterpret_cast<float4*>(out);
-#ifndef F16_DIAG_SKIP_COPYOUT
       for (int q = lane; q < n4; q += 64) {
 #if (IMG_OFF + F16_OBS_DIM) % 4 == 0
         out4[q] = reinterpret_cast<const float4*>(img + IMG_OFF + F16_OBS_DIM)[q];
@@ -856,7 +839,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         out4[q] = make_float4(p[0], p[1], p[2], p[3]);
 #endif
       }
-#endif
       for (int j = 4 * n4 + lane; j < total; j += 64) out[j] = img[IMG_OFF + j + F16_OBS_DIM];
     }
     F16_STAMP(stamps, ST_COPY);
