@@ -1123,11 +1123,17 @@ struct ResetDoneArgs {
 __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) {
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   if (a.zero_next && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_next = 0;
+  // one round trip before the work: the table DMA, the done count and this thread's first list
+  // entry in flight together (the list holds N entries, so the speculative read is in bounds)
+  stage_tables_issue(sT);
+  const int64_t i0 = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const int nd = *a.n_done;
-  if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // block-uniform: no barrier skipped by part of a block
-  stage_tables(sT);
-  for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < nd; i += (int64_t)gridDim.x * BLOCK) {
-    const int64_t k = a.done_idx[i];
+  const int32_t k0 = i0 < a.E.n ? a.done_idx[i0] : -1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // after the only barrier
+  for (int64_t i = i0; i < nd; i += (int64_t)gridDim.x * BLOCK) {
+    const int64_t k = i == i0 ? k0 : a.done_idx[i];
     if (k < 0 || k >= a.E.n) continue;
     Lane L;
     lane_load<true>(a.s, k, L);
