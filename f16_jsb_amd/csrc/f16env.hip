@@ -652,11 +652,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // Early state store, with no done list to compact (its atomic's return would wait for every
   // store before it): retire the stack DMA and store the state columns the frames left final
   // now, so their drain overlaps the observation frame, reward and obs writes instead of
-  // adding to the tail. Two-waves-per-SIMD builds (gpurun r02m, MODE 0: 131 072 envs 30.35 ->
-  // 29.89 us, 262 144 62.35 -> 60.0 us) and the one-wave non-temporal windowed build (65 536
-  // envs 16.85 -> 16.50 us over three same-box A/Bs, r02_variants_early_store.txt); the
-  // one-wave contiguous build gained nothing at 65 536 envs and lost 0.4 us at 4 096.
-  const bool early_store = (LOWREG || (WIN && NT)) && !a.done_idx;
+  // adding to the tail. Two-waves-per-SIMD builds only (gpurun r02m, MODE 0: 131 072 envs
+  // 30.35 -> 29.89 us, 262 144 62.35 -> 60.0 us). At one wave per SIMD: the contiguous build
+  // gained nothing at 65 536 envs and lost 0.4 us at 4 096; the non-temporal windowed build
+  // gained 0.35 us on fresh episodes but lost 0.3-0.4 us in the bench's steady state, where
+  // a lane reset by the step stores its row twice (r02_variants_early_store.txt).
+  const bool early_store = LOWREG && !a.done_idx;
   if (early_store) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (live) lane_store<GUST, 1, NT>(a.s, k, L);
