@@ -21,6 +21,9 @@ CASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4), (65536, 1
 WCASES = [(65536, 4, 4), (65536, 4, 0), (131072, 4, 4), (262144, 4, 4), (4096, 4, 4)]
 # cfg5 mode (random ICs + gusts: MODE 3 kernels), window layout
 C5CASES = [(131072, 4, 4), (65536, 4, 4)]
+# the bench headline's steady-state episode mix (bench.spread_phases: phase spread + burn-in),
+# window layout -- what a change must not lose (fresh episodes have no auto-resets)
+SCASES = [(65536, 4, 4)]
 
 
 def build(specs):
@@ -39,11 +42,16 @@ def run_one():
     import torch
     from f16_jsb_amd.env import F16Envs
     res = {}
-    runs = [("c", *c) for c in CASES] + [("w", *c) for c in WCASES] + [("w5", *c) for c in C5CASES]
+    runs = ([("c", *c) for c in CASES] + [("w", *c) for c in WCASES] + [("w5", *c) for c in C5CASES]
+            + [("ws", *c) for c in SCASES])
     for lay, n, k, ds in runs:
         e = F16Envs(n, stack_k=k, down_sample=ds, seed=1, obs_layout="contiguous" if lay == "c" else "window",
                     cfg5=lay == "w5")
         e.reset()
+        if lay == "ws":
+            import argparse
+            from bench import spread_phases
+            spread_phases(e, argparse.Namespace(seed=0, burn_in=None), e.device)
         acts = [e.sample_actions(5, t) for t in range(16)]
         for t in range(20):
             e.step(acts[t % 16])
