@@ -227,9 +227,11 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   Stamps stamps = {};
 #endif
   const AltRef A = alt_ref(L, ce, se);
-  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);  // three passes, as oracle apply_ic()
-  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
-  frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
+  // three passes, as oracle apply_ic(); a loop, not three inlined copies: the reset kernels run
+  // one RunIC per lane from a cold instruction cache, so one copy of the frame code is fetched
+  // once and hit twice
+#pragma nounroll
+  for (int pass = 0; pass < 3; ++pass) frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
   for (int j = 0; j < 3; ++j) { L.dv1[j] = 0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }
 }
 
