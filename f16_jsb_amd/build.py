@@ -29,8 +29,12 @@ def build(verbose: bool = False, force: bool = False, extra=()) -> str:
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= t_out for d in DEPS):
             return OUT
-    # -fno-slp-vectorize: packed-f32 pairing costs more v_mov than it saves at one wave/SIMD
+    # -fno-slp-vectorize: packed-f32 pairing costs more v_mov than it saves at one wave/SIMD.
+    # kernarg preload (gfx950): the first 8 argument dwords arrive in SGPRs at wave start; the
+    # windowed step kernels take their prologue's addresses there (StepPre): 65 536 envs kernel
+    # 16.51 -> 16.19 us (two same-box A/Bs, profiles/r02_variants_preload.txt)
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
+           "-mllvm", "-amdgpu-kernarg-preload-count=8",
            "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
            SRC, "-o", OUT + ".tmp", *extra]
     if verbose:

@@ -532,8 +532,19 @@ static constexpr int WFRESH = 16 * 64;  // LDS floats per wave for the fresh-fra
 static constexpr int WSTASH = 16 * 64;  // ... and for the env-field stash of the 256-register builds
 static constexpr int WIN_WAVE_FLOATS = WFRESH + WSTASH;
 
+// The prologue's first loads from kernel arguments preloaded into SGPRs (StepPre, windowed
+// kernels): the state, action and template addresses and N are in registers when the wave
+// starts, so the state / action loads and the table and template DMA issue without first
+// waiting for the scalar load of the argument block (-amdgpu-kernarg-preload-count, build.py).
+struct StepPre {
+  const float4* sc;
+  const float* act;
+  const float4* tmpl;
+  int64_t n;
+};
 template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false>
-__device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl) {
+__device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl,
+                                          const StepPre* pre = nullptr) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
 #ifdef F16_STAMPS
@@ -543,7 +554,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
-  const int rows = (int)(a.E.n - row0 < 64 ? (a.E.n - row0 > 0 ? a.E.n - row0 : 0) : 64);
+  const int64_t nE = pre ? pre->n : a.E.n;
+  const int rows = (int)(nE - row0 < 64 ? (nE - row0 > 0 ? nE - row0 : 0) : 64);
   const bool image = a.lds_image != 0;
 #ifdef F16_NO_STASH
   constexpr bool STASH = false;
@@ -565,7 +577,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     }
   };
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = k < a.E.n;
+  const bool live = k < nE;
   int done = 0;
   Lane L;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -576,11 +588,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   if (!GT) stage_tables_issue(sT_lds);
   // IC template: the NCOL state columns, then its frame-0 columns (lane i lands at sTmpl[i])
   if (!DEFER && threadIdx.x < NCOL + TMPL_FRAME_COLS)
-    dma16(reinterpret_cast<const float*>(a.tmpl.c + (threadIdx.x < NCOL ? threadIdx.x : threadIdx.x + NCOL_ALL - NCOL)),
+    dma16(reinterpret_cast<const float*>((pre ? pre->tmpl : a.tmpl.c) + (threadIdx.x < NCOL ? threadIdx.x : threadIdx.x + NCOL_ALL - NCOL)),
           reinterpret_cast<float*>(sTmpl));
   if (live) {
-    lane_load<GUST>(a.s, k, L);
-    if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
+    if (pre) {
+      const SoA sp = {const_cast<float4*>(pre->sc), pre->n};
+      lane_load<GUST>(sp, k, L);
+      av = reinterpret_cast<const float4*>(pre->act)[k];
+    } else {
+      lane_load<GUST>(a.s, k, L);
+      if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -945,19 +963,26 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
 // windowed-observation build (f16env_step_window): no stack image, LDS holds the tables and
 // the per-wave frame staging
 template <int MODE, int OCC>
-__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_kernel(const float4* __restrict__ sc, const float* __restrict__ act,
+                                                                  const float4* __restrict__ tmpl, int64_t n, StepArgs a) {
   STEP_SHARED
-  step_body<MODE, false, false, OCC == 2, true>(a, sT, sTmpl, sDone, dynl);
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, false, false, OCC == 2, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 // ... with non-temporal state and frame-slot stores, for grids resident in one round (st16)
 template <int MODE, int OCC>
-__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(const float4* __restrict__ sc,
+                                                                     const float* __restrict__ act,
+                                                                     const float4* __restrict__ tmpl, int64_t n,
+                                                                     StepArgs a) {
   STEP_SHARED
-  step_body<MODE, false, false, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl);
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, false, false, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 using StepKernel = void (*)(StepArgs);
-static StepKernel step_win_kernel_for(int mode, int occ, int nt) {
-  static const StepKernel table[2][2][4] = {
+using WinKernel = void (*)(const float4*, const float*, const float4*, int64_t, StepArgs);
+static WinKernel step_win_kernel_for(int mode, int occ, int nt) {
+  static const WinKernel table[2][2][4] = {
       {{f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
        {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}},
       {{f16_step_win_nt_kernel<0, 1>, f16_step_win_nt_kernel<1, 1>, f16_step_win_nt_kernel<2, 1>,
@@ -1975,12 +2000,16 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   int32_t* zero_next = nullptr;
   if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) return e;
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
-  const StepKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt);
+  const WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt);
+  const float4* sc = a.s.c;
+  const float4* tc = a.tmpl.c;
+  const int64_t n = a.E.n;
   if (h->prof_next < (int)h->prof_ev.size() / 2) {
     const int i = h->prof_next++;
-    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)WIN_DYN_LDS, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u, a);
+    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)WIN_DYN_LDS, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u,
+                          sc, act, tc, n, a);
   } else {
-    hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, a);
+    hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, sc, act, tc, n, a);
   }
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
