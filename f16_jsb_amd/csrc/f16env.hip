@@ -594,7 +594,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     if (pre) {
       const SoA sp = {const_cast<float4*>(pre->sc), pre->n};
       lane_load<GUST>(sp, k, L);
-      av = reinterpret_cast<const float4*>(pre->act)[k];
+      if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(pre->act)[k];
     } else {
       lane_load<GUST>(a.s, k, L);
       if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
@@ -943,22 +943,26 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
 // OCC = 2 caps it at 256 (a few spills) so two waves share each SIMD: slower per wave, but
 // when there are more waves than SIMDs (N > 64 x 4 x CUs) the pair overlaps one wave's
 // memory phases and stalls with the other's VALU work (f16env_step picks per launch).
-__global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(StepArgs a) {
+#define STEP_PRE_ARGS const float4 *__restrict__ sc, const float *__restrict__ act, const float4 *__restrict__ tmpl, int64_t n
+__global__ __launch_bounds__(BLOCK, 1) void f16_step_kernel(STEP_PRE_ARGS, StepArgs a) {
   STEP_SHARED
-  step_body<0>(a, sT, sTmpl, sDone, dynl);
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<0>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 template <int MODE, int OCC, bool ROLL = false>
-__global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_var_kernel(STEP_PRE_ARGS, StepArgs a) {
   STEP_SHARED
-  step_body<MODE, false, ROLL, OCC == 2>(a, sT, sTmpl, sDone, dynl);
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, false, ROLL, OCC == 2>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 // global-table variant (large K on the LDS-image path): no LDS table copy
 template <int MODE, bool ROLL = false>
-__global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(STEP_PRE_ARGS, StepArgs a) {
   __shared__ __align__(16) float4 sTmpl[NCOL + TMPL_FRAME_COLS];
   __shared__ int sDone[BLOCK];
   extern __shared__ __align__(16) float dynl[];
-  step_body<MODE, true, ROLL>(a, nullptr, sTmpl, sDone, dynl);
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, true, ROLL>(a, nullptr, sTmpl, sDone, dynl, &pre);
 }
 // windowed-observation build (f16env_step_window): no stack image, LDS holds the tables and
 // the per-wave frame staging
@@ -979,8 +983,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(const float
   const StepPre pre = {sc, act, tmpl, n};
   step_body<MODE, false, false, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
-using StepKernel = void (*)(StepArgs);
-using WinKernel = void (*)(const float4*, const float*, const float4*, int64_t, StepArgs);
+using StepKernel = void (*)(const float4*, const float*, const float4*, int64_t, StepArgs);
+using WinKernel = StepKernel;
 static WinKernel step_win_kernel_for(int mode, int occ, int nt) {
   static const WinKernel table[2][2][4] = {
       {{f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
@@ -1921,9 +1925,10 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   const StepKernel kern = step_kernel_for(h->mode, h->gt ? 2 : (h->occ == 2 ? 1 : 0), slot != nullptr);
   if (h->prof_next < (int)h->prof_ev.size() / 2) {  // profiling: events from the dispatch packet itself
     const int i = h->prof_next++;
-    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)h->dyn_lds, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u, a);
+    hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)h->dyn_lds, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u,
+                          (const float4*)a.s.c, a.act, (const float4*)a.tmpl.c, a.E.n, a);
   } else {
-    hipLaunchKernelGGL(kern, grid, blk, h->dyn_lds, st, a);
+    hipLaunchKernelGGL(kern, grid, blk, h->dyn_lds, st, (const float4*)a.s.c, a.act, (const float4*)a.tmpl.c, a.E.n, a);
   }
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
