@@ -14,7 +14,8 @@ Envs shard across ranks (weak scaling, no collective in the stepping loop); the 
 value is all ranks' env-steps divided by the max-over-ranks wall time.
 
 Prints ONE JSON line on rank 0 (driver contract), including
-  roofline     -- algorithmic HBM bytes per launch of the step kernel / its average launch
+  roofline     -- algorithmic HBM bytes per launch of the step kernel (the bytes its layout
+                  must move; SURVEY 8(d)'s B(K) beside it as contract_*) / its average launch
                   duration (HIP events on the launch stream), vs the 8 TB/s HBM peak;
                   `traffic` = PMC-measured HBM bytes per launch from profiles/ if present;
   cpu_baseline -- the CPU oracle (oracle/f16ref.c, fp64 C restatement, OpenMP) timed on this
@@ -24,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -75,11 +77,14 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
                 "sample": "oracle unavailable: %s" % e}
     import numpy as np
     threads = int(lib().f16ref_threads())
-    # the lease's CPU share: the threads OpenMP may use are the CPUs this process may run on
+    # CPUs this process may run on (on the GPU box: the whole machine; the lease's share is OMP_NUM_THREADS)
     affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     n = min(envs, 65536)
     e = OracleEnvs(n, stack_k=stack, seed=1, cfg5=cfg5)
     e.reset()
+    tw = time.perf_counter()  # untimed warm-up (thread pool, first touch of the env arrays)
+    while time.perf_counter() - tw < 0.5:
+        e.step(e.sample_actions(2, 0))
     steps = 0
     t0 = time.perf_counter()
     while True:
@@ -90,20 +95,34 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
         if el >= seconds or steps >= 2000:
             break
     e.close()
-    # SURVEY 8(d) also asks for the all-cores rate at N = 4096 (cfg2's env count): 3 s sample
-    n4 = None
-    if n > 4096:
+    # SURVEY 8(d) also asks for the all-cores rate at N = 4096 (cfg2's env count), and the rate
+    # against the thread count: 4 096 envs at 1, 2, 4, 8 ... threads up to the inherited count
+    def rate4096(nthreads, secs):
+        lib().f16ref_set_threads(nthreads)
         e4 = OracleEnvs(4096, stack_k=stack, seed=1, cfg5=cfg5)
         e4.reset()
+        for w in range(3):
+            e4.step(e4.sample_actions(2, w))
         s4 = 0
         t4 = time.perf_counter()
-        while time.perf_counter() - t4 < min(3.0, seconds):
+        while time.perf_counter() - t4 < secs:
             e4.step(e4.sample_actions(1, s4))
             s4 += 1
         el4 = time.perf_counter() - t4
         e4.close()
-        n4 = {"value": round(4096 * s4 / el4, 1), "unit": "env-steps/s", "cores": threads,
+        return round(4096 * s4 / el4, 1), s4, el4
+    scaling = {}
+    for nt in sorted({1, 2, 4, 8, threads}):
+        if nt <= threads:
+            scaling[str(nt)] = rate4096(nt, min(1.5, seconds))[0]
+    lib().f16ref_set_threads(0)
+    n4 = None
+    if n > 4096:
+        v4, s4, el4 = rate4096(threads, min(3.0, seconds))
+        lib().f16ref_set_threads(0)
+        n4 = {"value": v4, "unit": "env-steps/s", "cores": threads,
               "sample": "4096 envs x %d random-action steps, %.1f s" % (s4, el4)}
+    per_core = scaling[str(threads)] / threads
     # BASELINE cfg1 semantics beside it: ONE env, 1000 random-action steps, reference stack K=10
     e1 = OracleEnvs(1, stack_k=10, seed=1)
     e1.reset()
@@ -125,11 +144,18 @@ def cpu_baseline(envs, stack, seconds, cfg5=False):
         pass
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port", "cfg1": cfg1,
             "n4096": n4,
+            "thread_scaling_4096_envs": scaling,
+            "all_affinity_cpus_extrapolated": {
+                "value": round(per_core * affinity, 1), "cores": affinity, "measured": False,
+                "basis": "per-thread rate at %d threads (4096 envs) x %d CPUs of the affinity set, linear as "
+                         "thread_scaling_4096_envs is up to the share" % (threads, affinity),
+                "why_not_measured": "the GPU pool grants each 1-GPU lease a %s-CPU share and sets "
+                                    "OMP_NUM_THREADS to it (to be left as set); the affinity set is the whole "
+                                    "machine's CPUs, shared with other leases" % os.environ.get("OMP_NUM_THREADS")},
             "host": {"cpu_model": model, "os_cpu_count": os.cpu_count(), "sched_affinity_cpus": affinity,
                      "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-                     "cores_note": "cores = OpenMP threads used = min(OMP_NUM_THREADS, CPUs in this process's "
-                                   "affinity set); os_cpu_count is the whole machine, of which the GPU lease "
-                                   "grants the affinity set"},
+                     "cores_note": "cores = OpenMP threads used = OMP_NUM_THREADS (the lease's CPU share); "
+                                   "os_cpu_count / sched_affinity_cpus are the whole machine"},
             "sample": "oracle/f16ref.c (fp64 C restatement of the JSBSim F-16 FDM, not JSBSim), "
                       "%d envs x %d random-action steps (stack=%d, auto-reset%s), %d OpenMP threads, %.1f s"
                       % (n, steps, stack, ", cfg5 random IC + gusts" if cfg5 else "", threads, el)}
@@ -426,8 +452,9 @@ def layout_leg(dev, args, layout, steps=300):
     b, lb = e.stack_bytes_per_env_step(), e.algorithmic_bytes_per_env_step()
     out = {"layout": layout, "kernel": e.step_kernel_name, "region_ms_per_step": round(region, 5),
            "kernel_ms": round(kern_ms, 5), "env_steps_per_s_region": round(args.envs / (region * 1e-3), 1),
-           "algorithmic_bytes_per_env_step": b, "layout_bytes_per_env_step": lb,
-           "frac_of_hbm_peak": round(b * args.envs / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+           "algorithmic_bytes_per_env_step": lb, "contract_bytes_per_env_step": b,
+           "frac_of_hbm_peak": round(lb * args.envs / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+           "contract_frac": round(b * args.envs / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
     e.close()
     return out
 
@@ -503,17 +530,27 @@ def main():
     warm = torch.empty((max(args.warmup, 1), n, 4), dtype=torch.float32, device=dev)
     for t in range(args.warmup):
         envs.sample_actions(args.seed + 2000, t, out=warm[t])
+    from f16_jsb_amd.abi import F16C_EP_COUNT
+    stream = torch.cuda.current_stream(dev)
+    start_ev, end_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # The host operations between the warm-up and the timed region run once here first: the
+    # first launch after a new kind of runtime call (a first reduce kernel, a first event
+    # record, a fresh allocation) costs the host ~100 us (tools/driver_gap.py,
+    # profiles/r03_driver_gap.json), which lands in a 20-step region as ~5 us per step
+    envs.get_state()[:, F16C_EP_COUNT].sum()
+    start_ev.record(stream)
+    end_ev.record(stream)
+    torch.cuda.synchronize()
     for t in range(args.warmup):
         envs.step(warm[t])
     torch.cuda.synchronize()
 
-    from f16_jsb_amd.abi import F16C_EP_COUNT
     ep0 = envs.get_state()[:, F16C_EP_COUNT].sum()
-    stream = torch.cuda.current_stream(dev)
-    start_ev, end_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    gc.collect()
+    gc.disable()  # no collector pause inside the timed steps
     t0 = time.perf_counter()
     start_ev.record(stream)
     for t in range(args.steps):
@@ -523,6 +560,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     gpu_ms_per_step = start_ev.elapsed_time(end_ev) / args.steps
     # auto-resets inside the timed region, from the lanes' episode counters (read after it:
     # nothing is added to the timed loop)
@@ -561,11 +599,13 @@ def main():
         return
     total_env_steps = n * world * args.steps
     value = total_env_steps / elapsed
-    # algorithmic bytes: SURVEY.md 8(d)'s per-env-step figure B(K) (the step's contract: state
-    # read + written, action, reward, flags, a K-frame observation); the windowed layout meets
-    # that contract moving fewer bytes (its own count beside it, and the PMC traffic)
-    bytes_per_env_step = envs.stack_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
-    layout_bytes = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)
+    # roofline bytes: what this layout's step kernel must move per env step (window: state read
+    # + written, action, reward, flags and the new frame into both histories, 16 + 2*60 + 4 + 2
+    # + 2S; contiguous: SURVEY.md 8(d)'s B(K) with the stack read and rewritten). SURVEY's B(K)
+    # -- the step's contract with a materialised K-frame stack -- is reported beside it
+    # ("contract_*"): the windowed layout meets that contract without moving its extra bytes.
+    bytes_per_env_step = envs.algorithmic_bytes_per_env_step() + (24 if cfg5 else 0)  # + gust state r/w
+    contract_bytes = envs.stack_bytes_per_env_step() + (24 if cfg5 else 0)
     bytes_per_launch = bytes_per_env_step * n
     # launch duration used for the roofline: the kernel's average execution time from its own
     # dispatch events (what rocprofv3 --kernel-trace reports); the timed region's GPU time per
@@ -621,12 +661,12 @@ def main():
             "region_ms_per_launch": round(gpu_ms_per_step, 5),
             "region_timing": "HIP events around the timed region on the launch stream / launches",
             "algorithmic_bytes_per_env_step": bytes_per_env_step,
-            "bytes_basis": "SURVEY 8(d) B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S, S = %d" % envs.state_bytes_per_env,
-            # the bytes this layout's kernel must move for the same step (window: the new frame
-            # to both histories, no stack read / rewrite: 16 + 2*60 + 4 + 2 + 2S) and the HBM
-            # fraction they make over the same launch time
-            "layout_bytes_per_env_step": layout_bytes,
-            "layout_frac": round(layout_bytes * n / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "bytes_basis": ("%s layout: 16 (action) + 2 x 60 (new frame into both histories) + 4 + 2 + 2S, S = %d"
+                            % (args.obs_layout, envs.state_bytes_per_env) if envs.window else
+                            "SURVEY 8(d) B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S, S = %d" % envs.state_bytes_per_env),
+            # SURVEY 8(d)'s B(K), the bytes of the same step with the K-frame stack materialised
+            "contract_bytes_per_env_step": contract_bytes,
+            "contract_frac": round(contract_bytes * n / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
             "obs_layout": args.obs_layout,
             "launch_env_steps": n,
         },

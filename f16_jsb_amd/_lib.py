@@ -60,6 +60,7 @@ def lib():
     _set(L, "f16env_step_mode", [vp], i32)
     _set(L, "f16env_features_strided", [vp, i64, i32, vp, i64, i64, vp], i32)
     _set(L, "f16env_set_window_order", [vp, i32], i32)
+    _set(L, "f16env_window_clear_fresh", [vp, vp], i32)
     _set(L, "f16env_window_bind", [vp, vp, vp, i64, vp, vp, vp, vp, vp], i32)
     _set(L, "f16env_window_step_bound", [vp, vp, vp, i32, i32], i32)
     _set(L, "f16env_step_window_nt", [vp], i32)
@@ -73,7 +74,9 @@ def lib():
                              ctypes.c_double, vp, vp]
     L.f16env_features.argtypes = [vp, ctypes.c_int64, vp, vp]
     _set(L, "f16env_poses", [vp, ctypes.c_int64, vp, ctypes.c_int64, vp], i32)
+    L.f16env_step_kernel_name.argtypes = [vp]
     L.f16env_step_kernel_name.restype = ctypes.c_char_p
+    _set(L, "f16env_profile_times", [vp, ctypes.POINTER(ctypes.c_double), i32], i32)
     L.f16env_step_waves_per_simd.argtypes = [vp]
     L.f16env_step_waves_per_simd.restype = i32
     _set(L, "f16env_step_variant", [vp], i32)
@@ -102,9 +105,9 @@ EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
-    "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order",
+    "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order", "f16env_window_clear_fresh",
     "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt",
     "f16env_get_state",
-    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end",
+    "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end", "f16env_profile_times",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",
 )

@@ -325,8 +325,17 @@ __device__ __forceinline__ int env_reward(Lane& L, const float* f, const EnvArgs
     d2 = d2 + dy * dy;
     if (!te && sqrtf(d2) < E.dg && fabsf(alt - f[14]) < E.dg) { r = 10.0; te = 1; }
     tr = L.step >= E.max_steps ? 1 : 0;                   // env :260 | TimeLimit
+    // The previous distance is moved into a register of its own first. SROA keeps the Lane's
+    // {goal.z, last_d, wind.x, wind.y} as one 4-VGPR tuple, and the new distance below is
+    // written into the same tuple's last_d lane; in f16_step_win_nt_kernel<2|3, 1> (ROCm 7.2,
+    // LLVM 22) the register allocator then placed that write before the read of the old value
+    // (`v_sub_f32 v0, v207, v207`: every shaping term, hence every reward, was 0 -- the "all-zero
+    // rewards" of round 2). The empty asm breaks the tuple's live range; tests/test_isa_lint.py
+    // scans the built code object for x - x subtractions.
+    float last_d = L.last_d;
+    asm volatile("" : "+v"(last_d));
     const float dcur = norm3f(f[12] - f[0], f[13] - f[1], f[14] - f[2]);
-    const float ddiff = L.last_d - dcur;
+    const float ddiff = last_d - dcur;
     r = r + E.gain * (double)ddiff;
     L.last_d = dcur;
     L.ep_ret += r;                                         // monitor.py:96-99
@@ -368,6 +377,37 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
   } else {
     rng_goal(E.seed, gid, (uint32_t)ep, L.goal);
   }
+  L.ep_count = ep + 1;
+  L.step = 0;
+  L.ep_ret = 0.0;
+  L.flags |= LANE_FLAG_FRESH;
+  make_frame(L, 1.0, 0.0, alt_ref(L, 1.0, 0.0), f0);
+  L.last_d = norm3f(f0[12] - f0[0], f0[13] - f0[1], f0[14] - f0[2]);
+}
+
+// lane_reset for a kernel compiled for one MODE (the windowed step's in-step RunIC): the random
+// IC stays a register array (lane_reset selects between it and the global config IC through
+// one pointer, which puts both in scratch)
+template <int MODE>
+__device__ void lane_reset_mode(Lane& L, const EnvArgs& E, int64_t k, const float* T, const ModelConsts& C,
+                                float* f0) {
+  const int32_t ep = L.ep_count;
+  const uint64_t gid = (uint64_t)(E.id_base + k);
+  if (E.flags & F16_FLAG_GUSTS) {  // (MODE bit 1 is also set by steady wind alone)
+    float xi[3];
+    rng_normals(E.seed, gid, (uint32_t)ep, 0u, xi);
+    for (int j = 0; j < 3; ++j) L.gust[j] = E.gust_sigma * xi[j];
+  } else {
+    L.gust[0] = L.gust[1] = L.gust[2] = 0.0f;
+  }
+  if (MODE & 1) {
+    double ric[F16_IC_N];
+    rng_ic(E.seed, gid, (uint32_t)ep, E.ic_lo, E.ic_hi, ric);
+    apply_ic(L, ric, T, C);
+  } else {
+    apply_ic(L, E.ic_cfg, T, C);
+  }
+  rng_goal(E.seed, gid, (uint32_t)ep, L.goal);
   L.ep_count = ep + 1;
   L.step = 0;
   L.ep_ret = 0.0;
@@ -488,6 +528,10 @@ struct StepArgs {
   int64_t wrow;                // floats between positions (position-major: N * 16; env-major: 16)
   int64_t wenv;                // floats between envs (position-major: 16; env-major: T * 16)
   int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
+  // cfg5 modes, windowed layout: the reset cache (f16_ic_fill_kernel): per lane the state and
+  // frame 0 (without the goal) of its NEXT reset, ICC_COLS columns; c == nullptr: deferred
+  // resets by f16_reset_done_kernel instead
+  SoA icc;
   EnvArgs E;
   ModelConsts C;
 };
@@ -557,6 +601,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   const int64_t nE = pre ? pre->n : a.E.n;
   const int rows = (int)(nE - row0 < 64 ? (nE - row0 > 0 ? nE - row0 : 0) : 64);
   const bool image = a.lds_image != 0;
+  // cfg5 modes in the windowed layout reset finished lanes in the step (reset cache)
+  const bool in_step_reset = WIN && DEFER && a.icc.c != nullptr && !(a.E.flags & F16_FLAG_NO_AUTORESET);
 #ifdef F16_NO_STASH
   constexpr bool STASH = false;
 #else
@@ -725,21 +771,38 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (a.ep_len) a.ep_len[k] = L.step;
       if (!DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)) {
         lane_reset_template(L, sTmpl, a.E, k, f0);
+      } else if (in_step_reset) {
+        // cfg5 modes, windowed layout: the lane's next reset from the cache when it holds that
+        // episode's (tag: the cached row's episode count = this lane's + 1; a reset is a pure
+        // function of (seed, env id, episode), so any row with that tag is the one), else the
+        // full RunIC here (a lane that finished twice within one fill period)
+        if (__float_as_int(a.icc.c[(int64_t)15 * a.icc.n + k].w) == L.ep_count + 1) {
+          lane_load<GUST>(a.icc, k, L);
+#pragma unroll
+          for (int j = 0; j < TMPL_FRAME_COLS; ++j) {
+            const float4 v = a.icc.c[(int64_t)(NCOL_ALL + j) * a.icc.n + k];
+            f0[4 * j] = v.x; f0[4 * j + 1] = v.y; f0[4 * j + 2] = v.z; f0[4 * j + 3] = v.w;
+          }
+          f0[12] = L.goal[0]; f0[13] = L.goal[1]; f0[14] = L.goal[2];
+        } else {
+          lane_reset_mode<MODE>(L, a.E, k, sT, a.C, f0);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < F16_OBS_DIM; ++j) f0[j] = f[j];
       }
     }
     F16_STAMP(stamps, ST_RESET);
-    if (!early_store || (done && !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
+    if (!early_store || (done && (!DEFER || in_step_reset) && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
       lane_store<GUST, 0, NT>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
     else
       lane_store<GUST, 2, NT>(a.s, k, L);  // the rest
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
-  // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel
-  const bool autoreset = !DEFER && !(a.E.flags & F16_FLAG_NO_AUTORESET);
+  // deferred modes: f16_reset_done_kernel rewrites finished rows after this kernel, unless the
+  // windowed step resets them itself (in_step_reset)
+  const bool autoreset = (!DEFER || in_step_reset) && !(a.E.flags & F16_FLAG_NO_AUTORESET);
   // rollout slot frame = newest frame of obs_prev (what the policy acted on), for every lane
   if (ROLL && a.r_frame && rows > 0) {
     if (image) {
@@ -1179,6 +1242,33 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
   }
 }
 
+// cfg5 reset cache (windowed layout): a lane's next reset -- RunIC of its random IC, gust
+// start, goal, frame 0 -- is a pure function of (seed, global env id, episode), so it is
+// evaluated ahead, here, for every lane whose cached row is not the one of its next episode
+// (tag: the row's episode count = the lane's + 1), and the windowed step copies it into a
+// finished lane like MODE 0's template reset. Run every ICC_PERIOD windowed steps (and at the
+// first): the lanes that reset since the last fill are refilled; a lane that finishes again
+// before that runs its RunIC inside the step. Columns: NCOL_ALL state columns, then frame 0
+// without the goal (TMPL_FRAME_COLS).
+enum { ICC_COLS = NCOL_ALL + TMPL_FRAME_COLS };
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void f16_ic_fill_kernel(SoA s, SoA cache, EnvArgs E, ModelConsts C) {
+  __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
+  stage_tables(sT);
+  const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= E.n) return;
+  const int32_t ep = __float_as_int(s.c[(int64_t)15 * s.n + k].w);
+  if (__float_as_int(cache.c[(int64_t)15 * cache.n + k].w) == ep + 1) return;
+  Lane L;
+  L.ep_count = ep;
+  L.flags = 0;
+  float f0[F16_OBS_DIM];
+  lane_reset_mode<MODE>(L, E, k, sT, C, f0);
+  lane_store<true>(cache, k, L);
+  for (int j = 0; j < TMPL_FRAME_COLS; ++j)
+    cache.c[(int64_t)(NCOL_ALL + j) * cache.n + k] = make_float4(f0[4 * j], f0[4 * j + 1], f0[4 * j + 2], f0[4 * j + 3]);
+}
+
 struct ResetArgs {
   SoA s, tmpl;
   const uint8_t* mask;
@@ -1303,7 +1393,12 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int*
   L.pri = (float)o[F16C_PID_R_I]; L.prp = (float)o[F16C_PID_R_P]; L.ppi = (float)o[F16C_PID_P_I];
   L.ppp = (float)o[F16C_PID_P_P]; L.pyi = (float)o[F16C_PID_Y_I]; L.pyp = (float)o[F16C_PID_Y_P];
   L.n1 = (float)o[F16C_N1]; L.n2 = (float)o[F16C_N2];
-  L.flags = o[F16C_AUG] != 0.0 ? LANE_FLAG_AUG : 0;
+  // FRESH (the lane's other window history still lacks its reset frames) describes the
+  // handle's observation histories, not the physics state, so it survives a set_state: a
+  // reset -> set_state -> step sequence still fills the new window from the reset frame
+  // (f16env_window_clear_fresh drops it once the caller has written whole windows)
+  const bool fresh = sign_flag(s.c[(int64_t)15 * s.n + k].y);
+  L.flags = (o[F16C_AUG] != 0.0 ? LANE_FLAG_AUG : 0) | (fresh ? LANE_FLAG_FRESH : 0);
   for (int j = 0; j < F16L_N; ++j) L.lx[j] = (float)o[F16C_LX + j];
   L.lx[F16L_VC_KTS] = qc_from_vcas(o[F16C_LX + F16L_VC_KTS], C);
   L.last_d = (float)o[F16C_LAST_D]; L.step = (int32_t)o[F16C_STEP]; L.ep_ret = o[F16C_EP_RET];
@@ -1313,6 +1408,15 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int*
   bool w = false;
   for (int j = 0; j < 3; ++j) w = w || L.wst[j] != 0.0f || L.gust[j] != 0.0f;
   if (w) atomicOr(wind_any, 1);
+}
+
+// the caller wrote whole observation windows into both histories (F16Envs.set_obs): no lane
+// needs its window filled from a reset frame any more (the FRESH sign bit of column 15's y)
+__global__ void f16_clear_fresh_kernel(SoA s) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= s.n) return;
+  float* y = &s.c[(int64_t)15 * s.n + k].y;
+  *y = without_sign_flag(*y);
 }
 
 // Trim: Newton on (alpha, elevator cmd, throttle cmd), mirrors oracle trim_one()
@@ -1586,6 +1690,11 @@ struct f16env {
     int32_t* ep_len;
   } wb;
   SoA soa, tmpl;
+  // cfg5 modes, windowed layout: reset cache (f16_ic_fill_kernel), allocated at the first
+  // windowed step; refilled every icc_period windowed steps
+  SoA icc;
+  int64_t icc_steps;
+  int icc_period;
   ModelConsts C;
   size_t bytes;
   int lds_image;   // step kernel stack-rebuild mode (LDS image when it fits)
@@ -1717,6 +1826,10 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
            ((cfg->flags & F16_FLAG_RANDOM_IC) && (cfg->ic_lo[j] != 0.0 || cfg->ic_hi[j] != 0.0));
   h->mode = ((cfg->flags & F16_FLAG_RANDOM_IC) ? 1 : 0) | (((cfg->flags & F16_FLAG_GUSTS) || wind) ? 2 : 0);
   h->done_buf = nullptr;
+  h->icc.c = nullptr; h->icc.n = cfg->n_envs;
+  h->icc_steps = 0;
+  h->icc_period = 32;
+  if (getenv("F16ENV_ICC_PERIOD")) h->icc_period = atoi(getenv("F16ENV_ICC_PERIOD"));
   if (hipMalloc(&h->tmem, (size_t)TMPL_COLS * 16) != hipSuccess ||
       hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||
       hipMalloc((void**)&h->done_buf, sizeof(int32_t) * ((size_t)cfg->n_envs + 2)) != hipSuccess) {
@@ -1822,6 +1935,20 @@ int f16env_profile_end(f16env_t h, double* avg_ms, double* min_ms, int* launches
   return 0;
 }
 
+int f16env_profile_times(f16env_t h, double* t_ms, int max_launches) {
+  if (!h || !t_ms) return set_err(-1, "null argument");
+  const int n = h->prof_next < max_launches ? h->prof_next : max_launches;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipEventSynchronize(h->prof_ev[2 * i + 1]));
+    float a = 0.0f, b = 0.0f;
+    HIPCHK(hipEventElapsedTime(&a, h->prof_ev[0], h->prof_ev[2 * i]));
+    HIPCHK(hipEventElapsedTime(&b, h->prof_ev[0], h->prof_ev[2 * i + 1]));
+    t_ms[2 * i] = a;
+    t_ms[2 * i + 1] = b;
+  }
+  return n;
+}
+
 int f16env_destroy(f16env_t h) {
   if (!h) return 0;
   hipSetDevice(h->device);
@@ -1829,6 +1956,7 @@ int f16env_destroy(f16env_t h) {
   hipFree(h->tmem);
   hipFree(h->ic_dev);
   if (h->done_buf) hipFree(h->done_buf);
+  if (h->icc.c) hipFree(h->icc.c);
   hipFree(h->nonfinite);
   prof_free(h);
   delete h;
@@ -1913,6 +2041,7 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
     return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
   a.wx = a.wy = nullptr; a.wrow = a.wenv = 0; a.wpos = 0;
+  a.icc.c = nullptr; a.icc.n = 0;
   a.E = env_args(h);
   a.C = h->C;
   a.lds_image = h->lds_image;
@@ -2003,8 +2132,31 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   a.lds_image = 0;
   hipStream_t st = (hipStream_t)stream;
   int32_t* zero_next = nullptr;
-  if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) return e;
   const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
+  // cfg5 modes: finished lanes are reset inside the step from the reset cache (period 0 or
+  // F16ENV_ICC_PERIOD=0: the deferred f16_reset_done_kernel instead)
+  const bool cache = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period > 0;
+  a.icc.c = nullptr; a.icc.n = a.E.n;
+  if (cache) {
+    if (!h->icc.c) {
+      const size_t b = (size_t)ICC_COLS * 16 * (size_t)a.E.n;
+      if (hipMalloc((void**)&h->icc.c, b) != hipSuccess) { h->icc.c = nullptr; return set_err(-3, "hipMalloc(reset cache) failed"); }
+      HIPCHK(hipMemsetAsync(h->icc.c, 0, b, st));  // tag 0: no row valid yet
+      h->icc_steps = 0;
+    }
+    if (h->icc_steps % h->icc_period == 0) {
+      using FillKernel = void (*)(SoA, SoA, EnvArgs, ModelConsts);
+      static const FillKernel fill[4] = {f16_ic_fill_kernel<0>, f16_ic_fill_kernel<1>, f16_ic_fill_kernel<2>,
+                                         f16_ic_fill_kernel<3>};
+      hipLaunchKernelGGL(fill[h->mode & 3], grid, blk, 0, st, h->soa, h->icc, a.E, h->C);
+      HIPCHK(hipGetLastError());
+    }
+    ++h->icc_steps;
+    a.icc = h->icc;
+    if (n_done) HIPCHK(hipMemsetAsync(n_done, 0, sizeof(int32_t), st));  // the caller's done list only
+  } else if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) {
+    return e;
+  }
   const WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt);
   const float4* sc = a.s.c;
   const float4* tc = a.tmpl.c;
@@ -2017,7 +2169,7 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
     hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, sc, act, tc, n, a);
   }
   HIPCHK(hipGetLastError());
-  if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET)) {
+  if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && !cache) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
     r.obs_row = Q; r.obs_off = (int64_t)(pos - a.E.K + 1) * P; r.obs_pitch = P; r.obs_slot = WPITCH;
@@ -2146,6 +2298,13 @@ int f16env_set_state(f16env_t h, void* stream, const double* canon) {
   return 0;
 }
 
+int f16env_window_clear_fresh(f16env_t h, void* stream) {
+  if (!h) return set_err(-1, "null handle");
+  hipLaunchKernelGGL(f16_clear_fresh_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream, h->soa);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int f16env_trim(f16env_t h, void* stream, const double* ic_in, double* ic_out, double* residual_out) {
   if (!h || !ic_in || !ic_out) return set_err(-1, "null argument");
   hipLaunchKernelGGL(f16_trim_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, (hipStream_t)stream,
@@ -2214,7 +2373,22 @@ int f16env_poses(void* stream, int64_t n, const float* frames, int64_t frame_str
   return 0;
 }
 
-const char* f16env_step_kernel_name(void) { return "f16_step_kernel"; }
+// The step kernel instance a handle launches in its observation layout: the windowed one once
+// f16env_window_bind has been called, else the contiguous one (step_kernel_for's table).
+const char* f16env_step_kernel_name(f16env_t h) {
+  static thread_local char buf[64];
+  if (!h) return "";
+  if (h->wb.hist[0]) {
+    snprintf(buf, sizeof buf, "f16_step_win%s_kernel<%d, %d>", h->win_nt ? "_nt" : "", h->mode & 3, h->win_occ);
+  } else if (h->gt) {
+    snprintf(buf, sizeof buf, "f16_step_gt_kernel<%d>", h->mode & 3);
+  } else if ((h->mode & 3) == 0 && h->occ == 1) {
+    snprintf(buf, sizeof buf, "f16_step_kernel");
+  } else {
+    snprintf(buf, sizeof buf, "f16_step_var_kernel<%d, %d>", h->mode & 3, h->occ);
+  }
+  return buf;
+}
 int f16env_step_waves_per_simd(f16env_t h) { return h ? h->occ : 0; }
 int f16env_step_mode(f16env_t h) { return h ? h->mode : -1; }
 int f16env_step_variant(f16env_t h) { return h ? (h->gt ? 2 : (h->occ == 2 ? 1 : 0)) : -1; }

@@ -77,6 +77,9 @@ class F16Envs:
             raise F16EnvError("device must be a cuda (ROCm) device, got %s" % self.device)
         self.n = int(n_envs)
         self.k = int(stack_k)
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        self._raw_stream = raw if raw is not None else (lambda i: torch.cuda.current_stream(i).cuda_stream)
         flags = int(cfg_kw.pop("flags", 0)) | (0 if autoreset else F16_FLAG_NO_AUTORESET) \
             | (F16_FLAG_NAN_GUARD if nan_guard else 0)
         self.cfg: EnvConfig = config_default(n_envs=n_envs, stack_k=stack_k, seed=seed, env_id_base=env_id_base,
@@ -139,10 +142,12 @@ class F16Envs:
 
     # --------------------------------------------------------------------------------------
     def _stream(self):
-        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+        return ctypes.c_void_p(self._stream_int())
 
     def _stream_int(self) -> int:
-        return self.torch.cuda.current_stream(self.device).cuda_stream
+        """The caller's current stream on this device (the raw handle: 0.03 us, where
+        torch.cuda.current_stream() builds a Stream object per call, ~1.7 us)."""
+        return self._raw_stream(self._dev_index)
 
     def _window(self, other: int = 0):
         """(N, K, 15) view of the current (other=0) or other-parity history's window (views are
@@ -186,15 +191,8 @@ class F16Envs:
 
     @property
     def step_kernel_name(self) -> str:
-        mode = int(lib().f16env_step_mode(self._h))
-        if self.window:
-            nt = int(lib().f16env_step_window_nt(self._h)) == 1
-            return "f16_step_win%s_kernel<%d, %d>" % ("_nt" if nt else "", mode, self.waves_per_simd)
-        variant = int(lib().f16env_step_variant(self._h))
-        if variant == 2:
-            return "f16_step_gt_kernel<%d>" % mode
-        occ = 2 if variant == 1 else 1
-        return "f16_step_kernel" if (mode, occ) == (0, 1) else "f16_step_var_kernel<%d, %d>" % (mode, occ)
+        """The step kernel instance this handle launches (the symbol rocprofv3 reports)."""
+        return lib().f16env_step_kernel_name(self._h).decode()
 
     @property
     def state_bytes_per_env(self) -> int:
@@ -377,12 +375,19 @@ class F16Envs:
               "f16env_rollout_random")
         self._cur ^= 1
 
-    def profile_kernel(self, fn, launches: int):
+    def profile_kernel(self, fn, launches: int, times: Optional[list] = None):
         """Run fn() (which issues `launches` steps) with the step kernel's own dispatch events
-        recording each launch; returns (avg_ms, min_ms, launches timed)."""
+        recording each launch; returns (avg_ms, min_ms, launches timed). `times`, a list,
+        receives each launch's (start, stop) in ms from the first launch's start."""
         L = lib()
         check(L.f16env_profile_begin(self._h, int(launches)), "f16env_profile_begin")
         fn()
+        if times is not None:
+            buf = (ctypes.c_double * (2 * int(launches)))()
+            got = L.f16env_profile_times(self._h, buf, int(launches))
+            if got < 0:
+                check(got, "f16env_profile_times")
+            times.extend((buf[2 * i], buf[2 * i + 1]) for i in range(got))
         avg, mn, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         check(L.f16env_profile_end(self._h, ctypes.byref(avg), ctypes.byref(mn), ctypes.byref(cnt)), "f16env_profile_end")
         return avg.value, mn.value, cnt.value
@@ -415,6 +420,8 @@ class F16Envs:
         if self.window:
             self._window(0).copy_(o)
             self._window(1).copy_(o)
+            # both windows are whole now: lanes reset before this need no refill at the next step
+            check(lib().f16env_window_clear_fresh(self._h, self._stream()), "f16env_window_clear_fresh")
         else:
             self._obs[self._cur].copy_(o)
 

@@ -239,6 +239,11 @@ int f16env_window_restart(f16env_t h, void* stream, float* hist0, float* hist1, 
  * above; 1 env-major N x T x 16 (view strides T*16, 16, 1). Set before the first windowed call
  * and keep it: the histories must be laid out accordingly. */
 int f16env_set_window_order(f16env_t h, int env_major);
+/* The caller has written whole observation windows into both histories (e.g. an observation
+ * copied in after f16env_set_state): lanes reset since the last step stop refilling their next
+ * window from the reset frame. (A reset marks its lanes so that the next windowed step fills
+ * the other history's window; f16env_set_state keeps that mark.) */
+int f16env_window_clear_fresh(f16env_t h, void* stream);
 /* Waves per SIMD the windowed step kernel of this handle is built for (1 or 2), and whether it
  * is the non-temporal-store build (1: the whole grid resident in one round of waves). */
 int f16env_step_window_waves_per_simd(f16env_t h);
@@ -293,7 +298,9 @@ int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);
 
 /* Canonical state export/import: canon is N x F16C_N double (device). The latch's p/q/r-aero
  * and ground speed are recomputed from the state on import (they are functions of it);
- * set_state waits for `stream` (it reads back whether any lane carries wind). */
+ * set_state waits for `stream` (it reads back whether any lane carries wind). The windowed
+ * layout's per-lane "reset since the last step" mark is not part of the canonical state and
+ * is kept by set_state (see f16env_window_clear_fresh). */
 int f16env_get_state(f16env_t h, void* stream, double* canon);
 int f16env_set_state(f16env_t h, void* stream, const double* canon);
 
@@ -340,9 +347,12 @@ int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float
  *           position in viewer axes (-gy, gz, gx) * 1e-3. */
 int f16env_poses(void* stream, int64_t n, const float* frames, int64_t frame_stride, float* out);
 
-/* Name of the kernel symbol that dominates a step (for profilers), and the algorithmic
- * HBM bytes one env-step moves. */
-const char* f16env_step_kernel_name(void);
+/* Name of the step kernel instance the handle launches (for profilers: the symbol rocprofv3
+ * reports), e.g. "f16_step_win_nt_kernel<0, 1>" once f16env_window_bind was called (windowed
+ * layout), else the contiguous-layout instance; it changes when set_state / a per-lane IC
+ * switches the handle to the wind kernels. And the algorithmic HBM bytes one env-step moves
+ * (SURVEY.md 8d B(K)). */
+const char* f16env_step_kernel_name(f16env_t h);
 /* Waves per SIMD the handle's step kernel is built for: 1 (up to 64 x 4 x CUs envs), or 2
  * when there are more waves than SIMDs (override: env F16ENV_OCC=1|2 at create). */
 int f16env_step_waves_per_simd(f16env_t h);
@@ -360,6 +370,10 @@ double f16env_algorithmic_bytes_per_env_step(int stack_k);
  * kernel-trace average measures the same interval). */
 int f16env_profile_begin(f16env_t h, int max_launches);
 int f16env_profile_end(f16env_t h, double* avg_ms, double* min_ms, int* launches);
+/* Between f16env_profile_begin and _end: the start / stop time (ms) of each profiled launch
+ * relative to the first launch's start, t_ms[2i] / t_ms[2i+1] (waits for them). Returns the
+ * number of launches filled (<= max_launches), so gaps between launches can be read off. */
+int f16env_profile_times(f16env_t h, double* t_ms, int max_launches);
 
 const char* f16env_last_error(void);
 

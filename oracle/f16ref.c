@@ -1028,6 +1028,19 @@ int f16ref_threads(void) {
   return 1;
 #endif
 }
+/* thread count of the following parallel loops (bench.py's CPU-baseline core scaling); n <= 0
+ * restores the OMP_NUM_THREADS default */
+int f16ref_set_threads(int n) {
+#ifdef _OPENMP
+  static int dflt = 0;
+  if (!dflt) dflt = omp_get_max_threads();
+  omp_set_num_threads(n > 0 ? n : dflt);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
+}
 
 int f16ref_reset(f16ref* h, const uint8_t* mask, const float* goals, const double* ic, float* obs) {
   const int KO = h->cfg.stack_k * F16_OBS_DIM;

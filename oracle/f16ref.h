@@ -71,6 +71,7 @@ double f16ref_aero_scale(double in, double inmin, double inmax, double outmin, d
 double f16ref_seek(double v, double target, double accel, double decel, double dt);
 /* Number of OpenMP threads the batch loops use (1 if built without OpenMP). */
 int f16ref_threads(void);
+int f16ref_set_threads(int n);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,8 @@ def lib():
         L.f16ref_aero_table.restype = dp
         L.f16ref_n_aero_fns.restype = i32
         L.f16ref_threads.restype = i32
+        L.f16ref_set_threads.argtypes = [i32]
+        L.f16ref_set_threads.restype = i32
         L.f16ref_set_physics_mask.argtypes = [i32]
         L.f16ref_get_physics_mask.restype = i32
         L.f16ref_mass_props.argtypes = [vp, vp]

@@ -41,7 +41,7 @@ def test_library_loads_without_gpu(so_path):
         assert hasattr(L, name)
     assert set(_lib.EXPORTED_SYMBOLS) == set(declared_functions())
     # pure functions need no device
-    assert L.f16env_step_kernel_name() == b"f16_step_kernel"
+    assert L.f16env_step_kernel_name(None) == b""  # no handle, no kernel
     s = L.f16env_state_bytes_per_env()
     assert 200 <= s <= 400
     assert L.f16env_algorithmic_bytes_per_env_step(4) == 16 + 60 * 4 + 60 * 3 + 4 + 2 + 2 * s
@@ -96,6 +96,7 @@ def test_null_handle_calls_return_errors(so_path):
     assert L.f16env_step_window_nt(None) == -1
     assert L.f16env_step_window_waves_per_simd(None) == 0
     assert L.f16env_step_window(None, None, None, None, None, 8, 3, None, None, None, None, None, None, None) < 0
+    assert L.f16env_profile_times(None, None, 4) < 0
     assert L.f16env_window_restart(None, None, None, None, 8, 7) < 0
     assert L.f16env_reset_window(None, None, None, None, None, None, 8, 3) < 0
     # features on a strided block: bad shapes / strides are refused before any launch

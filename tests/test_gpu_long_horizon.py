@@ -51,10 +51,10 @@ def _kind(term, trunc, rew):
     return k
 
 
-def collect(n=N, steps=STEPS, seed=SEED, cfg5=False):
+def collect(n=N, steps=STEPS, seed=SEED, cfg5=False, layout="contiguous"):
     from f16_jsb_amd.env import F16Envs
     goals = _goals(n, seed)
-    sides = {"gpu": F16Envs(n, stack_k=K, seed=seed, max_steps=MAX_STEPS, cfg5=cfg5),
+    sides = {"gpu": F16Envs(n, stack_k=K, seed=seed, max_steps=MAX_STEPS, cfg5=cfg5, obs_layout=layout),
              "ref": OracleEnvs(n, stack_k=K, seed=seed, max_steps=MAX_STEPS, cfg5=cfg5)}
     out = {}
     for name, e in sides.items():
@@ -119,9 +119,12 @@ def statistics(out):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["contiguous", "window"])
 @pytest.mark.parametrize("cfg5", [False, True], ids=["reference_task", "cfg5"])
-def test_long_horizon_statistics(gpu, cfg5):
-    s = statistics(collect(cfg5=cfg5))
+def test_long_horizon_statistics(gpu, cfg5, layout):
+    """Both observation layouts: the windowed step kernels (the bench's) are separate template
+    instances of the same physics and must give the same episode statistics."""
+    s = statistics(collect(cfg5=cfg5, layout=layout))
     print(s)
     assert s["first_episode_agree"] >= 0.99, s
     # crashes and truncations recur by the thousand; goal captures are rarer under random

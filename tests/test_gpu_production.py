@@ -73,9 +73,11 @@ def _assert_frames_stat(gpu, ref, tol, tol_max, what):
     assert bad.size == 0, "%s: 99.9th percentile of component %d = %.3e > %.1e" % (what, bad[0], p[bad[0]], tol[bad[0]])
 
 
-def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None, early=None):
+def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None, early=None, done_list=True):
     """early = (step, tol): every lane's newest frame within tol at that step (before the
-    chaotic growth of the fp32-vs-fp64 difference sets in)."""
+    chaotic growth of the fp32-vs-fp64 difference sets in). done_list False: step exactly as
+    bench.py does (no caller done list: the windowed handle's bound five-argument launch, and
+    in cfg5 modes the handle's own done list + f16_reset_done_kernel), done flags still checked."""
     tol_max = tol_final if tol_max is None else tol_max
     n = ref.n
     done_idx = torch.zeros(n, dtype=torch.int32, device=g.device)
@@ -84,16 +86,20 @@ def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None,
     for t in range(1, steps + 1):
         a = ref.sample_actions(seed, t)
         o_r, r_r, te_r, tr_r, tobs_r, eret_r, elen_r = ref.step(a)
-        out = g.step(g.sample_actions(seed, t), done_idx=done_idx, n_done=n_done)
+        if done_list:
+            out = g.step(g.sample_actions(seed, t), done_idx=done_idx, n_done=n_done)
+        else:
+            out = g.step(g.sample_actions(seed, t))
         te_g = out.terminated.cpu().numpy().astype(bool)
         tr_g = out.truncated.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te_g, te_r, err_msg="terminated @%d" % t)
         np.testing.assert_array_equal(tr_g, tr_r, err_msg="truncated @%d" % t)
         np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3, err_msg="reward @%d" % t)
         d = te_r | tr_r
-        nd = int(n_done.item())
-        np.testing.assert_array_equal(np.sort(done_idx[:nd].cpu().numpy()), np.flatnonzero(d),
-                                      err_msg="done list @%d" % t)
+        if done_list:
+            nd = int(n_done.item())
+            np.testing.assert_array_equal(np.sort(done_idx[:nd].cpu().numpy()), np.flatnonzero(d),
+                                          err_msg="done list @%d" % t)
         if d.any():
             finished += int(d.sum())
             np.testing.assert_array_equal(out.ep_len.cpu().numpy()[d], elen_r[d])
@@ -115,34 +121,48 @@ def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None,
     return finished
 
 
-def test_cfg3_headline_instance_65536(torch_mod):
-    """BASELINE cfg3: 65 536 envs, K = 4, the headline kernel (f16_step_kernel, one wave per
-    SIMD, LDS tables, template auto-reset), 30 random-action steps vs the oracle."""
+# (layout, caller done list): the contiguous layout with the caller's done list (ABI coverage of
+# the compaction at production size), and the windowed layout exactly as bench.py steps it --
+# the bound launch without a done list -- i.e. the kernel instances behind the published numbers
+LAYOUTS = [("contiguous", True), ("window", False)]
+
+
+@pytest.mark.parametrize("layout,done_list", LAYOUTS, ids=[l for l, _ in LAYOUTS])
+def test_cfg3_headline_instance_65536(torch_mod, layout, done_list):
+    """BASELINE cfg3: 65 536 envs, K = 4, the headline kernels (one wave per SIMD, LDS tables,
+    template auto-reset): f16_step_kernel (contiguous) and f16_step_win_nt_kernel<0, 1> (window,
+    the bench headline), 30 random-action steps vs the oracle (jsbsim_gym.py:199-287)."""
     torch = torch_mod
     from f16_jsb_amd.env import F16Envs
     n = 65536
-    ref, g = OracleEnvs(n, stack_k=4, seed=31), F16Envs(n, stack_k=4, seed=31)
-    assert g.step_kernel_name == "f16_step_kernel" and g.waves_per_simd == 1
+    ref, g = OracleEnvs(n, stack_k=4, seed=31), F16Envs(n, stack_k=4, seed=31, obs_layout=layout)
+    want = "f16_step_win_nt_kernel<0, 1>" if layout == "window" else "f16_step_kernel"
+    assert g.step_kernel_name == want and g.waves_per_simd == 1, g.step_kernel_name
     o = ref.reset()
     o_g = g.reset().cpu().numpy()
     np.testing.assert_array_equal(o_g[:, :, 12:], o[:, :, 12:])
     _assert_frames(o_g[:, -1], o[:, -1], TOL_STEP, "reset")
     _stagger(ref, g, o)
-    fin = _run_parity(torch, ref, g, 30, 17, TOL_RAND30)
+    fin = _run_parity(torch, ref, g, 30, 17, TOL_RAND30, done_list=done_list)
     assert fin >= n // 3
+    assert g.step_kernel_name == want
     ref.close()
     g.close()
 
 
-def test_cfg5_production_instance_131072(torch_mod):
+@pytest.mark.parametrize("layout,done_list", LAYOUTS, ids=[l for l, _ in LAYOUTS])
+def test_cfg5_production_instance_131072(torch_mod, layout, done_list):
     """BASELINE cfg5 per-GPU share (1 048 576 / 8): 131 072 envs select the 256-register
-    two-waves-per-SIMD build f16_step_var_kernel<3, 2> and the deferred f16_reset_done_kernel
-    (random-IC RunIC + gust start). 30 random-action steps with gusts vs the oracle."""
+    two-waves-per-SIMD builds f16_step_var_kernel<3, 2> (contiguous) / f16_step_win_nt_kernel<3, 2>
+    (window, the cfg5 bench) and the deferred f16_reset_done_kernel (random-IC RunIC + gust
+    start). 30 random-action steps with gusts vs the oracle."""
     torch = torch_mod
     from f16_jsb_amd.env import F16Envs
     n = 131072
-    ref, g = OracleEnvs(n, stack_k=4, seed=41, cfg5=True), F16Envs(n, stack_k=4, seed=41, cfg5=True)
-    assert g.step_kernel_name == "f16_step_var_kernel<3, 2>", g.step_kernel_name
+    ref = OracleEnvs(n, stack_k=4, seed=41, cfg5=True)
+    g = F16Envs(n, stack_k=4, seed=41, cfg5=True, obs_layout=layout)
+    want = "f16_step_win_nt_kernel<3, 2>" if layout == "window" else "f16_step_var_kernel<3, 2>"
+    assert g.step_kernel_name == want, g.step_kernel_name
     assert g.waves_per_simd == 2
     o = ref.reset()
     o_g = g.reset().cpu().numpy()
@@ -158,8 +178,9 @@ def test_cfg5_production_instance_131072(torch_mod):
     # 131 072 lanes at step 30 p 3.0e-3 rad/s, r 3.2e-3, phi 2.7e-4 rad, beta 1.9e-4; at step
     # 10 p 3.6e-6. The one-wave build (F16ENV_OCC=1) and a second handle are bit-identical.
     fin = _run_parity(torch, ref, g, 30, 23, TOL_RAND30 * 2, gust=True, tol_max=TOL_RAND30 * 10,
-                      early=(10, TOL_RAND30))
+                      early=(10, TOL_RAND30), done_list=done_list)
     assert fin >= n // 3
+    assert g.step_kernel_name == want
     ref.close()
     g.close()
 

@@ -93,8 +93,16 @@ def test_window_two_waves_per_simd(gpu, monkeypatch):
     _run(a, b, 30)
 
 
-def test_window_cfg5_deferred_resets(gpu):
-    """cfg5 modes: random IC + gusts, resets by f16_reset_done_kernel into the window."""
+@pytest.mark.parametrize("period", ["0", "1", "32"])
+def test_window_cfg5_deferred_resets(gpu, monkeypatch, period):
+    """cfg5 modes: random IC + gusts. The windowed step resets finished lanes itself from the
+    reset cache (f16_ic_fill_kernel every `period` steps; a lane that finishes twice within a
+    period runs its RunIC in the step): period 1 -- every reset a cache hit; 32 -- with
+    max_steps 5, hits and in-step RunICs; 0 -- the deferred f16_reset_done_kernel instead.
+    Against the contiguous layout's deferred resets: identical done flags, values to fp32
+    rounding. (Round 2's all-zero rewards of this kernel instance were a register-allocation
+    miscompile, see tests/test_isa_lint.py.)"""
+    monkeypatch.setenv("F16ENV_ICC_PERIOD", period)
     a, b = _pair(512, 4, 8, max_steps=5, cfg5=True)
     assert b.step_kernel_name == "f16_step_win_nt_kernel<3, 1>"
     assert _run(a, b, 30) > 512
@@ -130,6 +138,21 @@ def test_window_set_state_and_obs(gpu):
     b.set_obs(a.obs)
     for t in range(6, 40):
         act = a.sample_actions(2, t)
+        _compare(a.step(act), b.step(act), t)
+
+
+@pytest.mark.parametrize("cfg5", [False, True], ids=["reference_task", "cfg5"])
+def test_window_reset_then_set_state_keeps_fresh(gpu, cfg5):
+    """reset -> set_state(get_state()) -> steps, with no set_obs (bench.py's spread_phases
+    sequence): the windowed handle keeps each lane's "reset since the last step" mark across
+    set_state, so the first observation after it carries K-1 copies of the reset frame, as the
+    contiguous layout's does (a fresh handle's other history is still all zeros)."""
+    a, b = _pair(700, 4, 16, max_steps=50, cfg5=cfg5)
+    np.testing.assert_array_equal(_np(b.reset()), _np(a.reset()))
+    a.set_state(a.get_state())
+    b.set_state(b.get_state())
+    for t in range(1, 13):
+        act = a.sample_actions(5, t)
         _compare(a.step(act), b.step(act), t)
 
 

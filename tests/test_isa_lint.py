@@ -1,0 +1,54 @@
+"""Static checks of the built gfx950 code object (CPU; no GPU needed).
+
+Round 2 recorded all-zero rewards from f16_step_win_nt_kernel<3, 1> whenever the step kernel
+carried a run-time reset path. Round 3 found the cause in the ISA: the shaping term
+r += 0.01 (last_d - d) of PositionReward (jsbsim_gym.py:493-507) compiled to
+`v_sub_f32 v0, v207, v207` -- the register allocator wrote the new distance into the tuple
+register that still held the previous one before reading it (a backend miscompile of ROCm 7.2's
+LLVM; the source workaround is in env_reward, f16env.hip). No source expression of the library
+subtracts a value from itself, so any `v_sub_f32 vX, vY, vY` in the code object is that bug
+again; the test disassembles every kernel and fails on one.
+"""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+LLVM_OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def _disassemble(so_path: str) -> str:
+    d = tempfile.mkdtemp(prefix="f16isa_")
+    try:
+        lib = os.path.join(d, "lib.so")
+        shutil.copy(so_path, lib)
+        subprocess.run([LLVM_OBJDUMP, "--offloading", lib], cwd=d, check=True, capture_output=True)
+        co = [f for f in os.listdir(d) if "gfx950" in f]
+        assert co, "no gfx950 code object in %s" % so_path
+        return subprocess.run([LLVM_OBJDUMP, "-d", "--no-show-raw-insn", os.path.join(d, co[0])],
+                              check=True, capture_output=True, text=True).stdout
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="ROCm llvm-objdump not present")
+def test_no_self_subtraction_in_step_kernels():
+    from f16_jsb_amd.build import build
+    asm = _disassemble(build())
+    kernel = None
+    bad = []
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            kernel = m.group(1)
+            continue
+        if re.search(r"\bv_sub_f32(_e32|_e64)?\s+v\d+, (v\d+), \2(\s|$)", line):
+            bad.append((kernel, line.strip()))
+    assert not bad, "x - x subtraction(s) in the code object (register-allocation miscompile): %s" % bad[:4]
+    # the step kernels are in there at all (the scan saw the real code)
+    assert "f16_step_win_nt_kernel" in asm and "f16_step_kernel" in asm

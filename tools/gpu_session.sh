@@ -27,15 +27,37 @@ run() {  # run <name> <timeout> <cmd...>
   return 0
 }
 
+run_abs() {  # run_abs <name> <timeout> <cmd...>: as run, from any working directory
+  local name=$1 lim=$2
+  shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$lim" "$@" > "$R/$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[session] $name rc=$rc"
+  tail -5 "$R/$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "[session] stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+  return 0
+}
+R=$(pwd)
+
 python -c "from f16_jsb_amd.build import build; build()" || exit 3
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests) run pytest_gpu_$TAG 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     prodtests) run pytest_prod 600 python -u -m pytest tests/test_gpu_production.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    smoke) run smoke_$TAG 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 50 ;;
+    driver) run bench_driver_$TAG 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    profdrv)  # rocprofv3 summary of the driver's exact command
+      (cd /tmp && run_abs prof_drv_$TAG 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/prof_drv_$TAG" -o run --output-format csv -- \
+        python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5) || exit $? ;;
+    gap) run driver_gap_$TAG 300 python tools/driver_gap.py --json "$OUT/driver_gap_$TAG.json" ;;
+    probe) run cp_pingpong_$TAG 120 tools/probes/cp_pingpong 2000 ;;
     stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
-    bench5) run bench_cfg5 600 python bench.py --workload cfg5 --steps 300 --warmup 20 --cpu-seconds 5 ;;
+    bench5) run bench_cfg5_$TAG 600 python bench.py --workload cfg5 --steps 300 --warmup 20 --cpu-seconds 5 ;;
     variants) run variant_sweep 900 python tools/variant_sweep.py run --json "$OUT/variants_$TAG.json" ;;
     div) run cfg5_divergence 900 python tests/cfg5_divergence.py --n 4096 --json "$OUT/cfg5_divergence_$TAG.json" ;;
     sweep) run kernel_sweep 600 python tools/kernel_sweep.py --json "$OUT/sweep_$TAG.json" ;;
