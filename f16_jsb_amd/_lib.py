@@ -66,6 +66,8 @@ def lib():
     _set(L, "f16env_step_window_nt", [vp], i32)
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_nonfinite_count.argtypes = [vp, vp, ctypes.POINTER(u64)]
+    _set(L, "f16env_obs_bounds_count", [vp, vp, ctypes.POINTER(u64)], i32)
+    _set(L, "f16env_debug_checks", [vp, vp, ctypes.POINTER(ctypes.c_uint32)], i32)
     L.f16env_rollout_random.argtypes = [vp, vp, u64, u64, i32] + [vp] * 7
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
@@ -103,7 +105,7 @@ def check(status: int, what: str):
 # symbols include/f16env.h declares (tests check the .so exports every one of them)
 EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
-    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_rollout_random",
+    "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_obs_bounds_count", "f16env_debug_checks", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
     "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order", "f16env_window_clear_fresh",
     "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt",

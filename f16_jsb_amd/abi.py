@@ -37,6 +37,7 @@ F16_FLAG_NO_AUTORESET = 0x1
 F16_FLAG_RANDOM_IC = 0x2  # cfg5: reset IC drawn from the [ic_lo, ic_hi] box
 F16_FLAG_GUSTS = 0x4      # cfg5: Gauss-Markov gusts on top of the steady wind
 F16_FLAG_NAN_GUARD = 0x8  # quarantine lanes whose frame goes non-finite (terminated = 3, counted)
+F16_FLAG_OBS_CHECK = 0x10  # count lane-steps whose new frame has a finite value outside the obs space
 
 # jsbsim_gym.py:28-53 observation bounds (per frame)
 EPSILON = 1e-5

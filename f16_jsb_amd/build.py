@@ -13,6 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "f16env.hip")
 OUT = os.path.join(HERE, "libf16env.so")
+# debug build: the same kernels with the F16_CHECK index / range invariants
+# compiled in (f16_device.h), read back by f16env_debug_checks; tests load it by F16ENV_LIB
+OUT_DEBUG = os.path.join(HERE, "libf16env_debug.so")
 DEPS = [SRC, os.path.join(HERE, "csrc", "f16_device.h"), os.path.join(HERE, "csrc", "f16_tables.h"),
         os.path.join(ROOT, "include", "f16env.h")]
 
@@ -24,11 +27,14 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build(verbose: bool = False, force: bool = False, extra=()) -> str:
-    if not force and os.path.exists(OUT):
-        t_out = os.path.getmtime(OUT)
+def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = False) -> str:
+    out = OUT_DEBUG if debug else OUT
+    if debug:
+        extra = tuple(extra) + ("-DF16_DEBUG_CHECKS",)
+    if not force and os.path.exists(out):
+        t_out = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= t_out for d in DEPS):
-            return OUT
+            return out
     # -fno-slp-vectorize: packed-f32 pairing costs more v_mov than it saves at one wave/SIMD.
     # kernarg preload (gfx950): the first 8 argument dwords arrive in SGPRs at wave start; the
     # windowed step kernels take their prologue's addresses there (StepPre): 65 536 envs kernel
@@ -36,13 +42,13 @@ def build(verbose: bool = False, force: bool = False, extra=()) -> str:
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
            "-mllvm", "-amdgpu-kernarg-preload-count=8",
            "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
-           SRC, "-o", OUT + ".tmp", *extra]
+           SRC, "-o", out + ".tmp", *extra]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv))
+    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv, debug="--debug" in sys.argv))

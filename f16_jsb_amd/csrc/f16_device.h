@@ -18,6 +18,32 @@
 
 namespace f16 {
 
+// Debug build (-DF16_DEBUG_CHECKS, build.py debug=True -> libf16env_debug.so):
+// index / range invariants the kernels rely on are checked at run time and violations are
+// recorded as bits of a device word (f16env_debug_checks reads it). A check never traps: a
+// fault or abort on the GPU box would take the box down, a recorded bit fails a test instead.
+// The product build compiles every F16_CHECK to nothing.
+enum DebugBits {
+  DBG_STATE_INDEX = 1,    // a lane index outside [0, n) reached a state access
+  DBG_WINDOW_POS = 2,     // a window slot position outside [0, T)
+  DBG_DONE_LIST = 4,      // the compacted done list overran N entries
+  DBG_TABLE_SEGMENT = 8,  // a table bracket outside its breakpoint vector
+  DBG_RESET_INDEX = 16,   // a deferred-reset list entry outside [0, n)
+  DBG_RING_SLOT = 32,     // a rollout ring slot outside [0, K)
+  DBG_FRAME_INDEX = 64,   // a features / poses frame index outside the block
+};
+#ifdef F16_DEBUG_CHECKS
+__device__ unsigned int g_f16_violations;
+#define F16_CHECK(cond, bit)                                   \
+  do {                                                         \
+    if (!(cond)) atomicOr(&::f16::g_f16_violations, (bit));    \
+  } while (0)
+#else
+#define F16_CHECK(cond, bit) \
+  do {                       \
+  } while (0)
+#endif
+
 // Diagnostic build only (-DF16_STAMPS): per-wave cycle totals per code section, from
 // s_memtime (a shader-clock counter), accumulated in scalar registers and stored once per
 // wave by lane 0. The production build compiles every F16_STAMP to nothing.
@@ -374,6 +400,7 @@ __device__ __forceinline__ Seg bracket(const float (&bp)[N], const float* pairs,
   for (int k = 1; k < N - 1; ++k) c += __float_as_uint(bp[k] - x) >> 31;
   const int i = 1 + (int)c;
 #endif
+  F16_CHECK(i >= 1 && i <= N - 1, DBG_TABLE_SEGMENT);
   const float2 p = reinterpret_cast<const float2*>(pairs)[i - 1];
   float f = (x - p.x) * p.y;
   f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
@@ -384,6 +411,7 @@ __device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, i
   const float u = (x - x0) * inv_h;
   int i = (int)floorf(u) + 1;
   i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
+  F16_CHECK(i >= 1 && i <= n - 1, DBG_TABLE_SEGMENT);
   float f = u - (float)(i - 1);
   f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
   return {i, f};

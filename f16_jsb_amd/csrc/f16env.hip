@@ -287,6 +287,19 @@ __device__ __forceinline__ float norm3f(float a, float b, float c) {
   return sqrtf(s);
 }
 
+// observation_space.contains on one frame, finite values only (jsbsim_gym.py:268-285 against
+// SINGLE_OBS_LOW / SINGLE_OBS_HIGH, :28-53, float32 bounds): a component outside its bounds
+// that is finite. (The infinite bounds of the other components admit every finite value.)
+__device__ __forceinline__ bool obs_out_of_bounds(const float* f) {
+  const float pe = (float)(PI_D + 1e-5), he = (float)(0.5 * PI_D + 1e-5);
+  bool bad = f[3] < 0.0f;                                 // mach >= 0
+  bad = bad || f[4] < -pe || f[4] > pe || f[5] < -pe || f[5] > pe;  // alpha, beta
+  bad = bad || f[9] < -pe || f[9] > pe || f[11] < -pe || f[11] > pe;  // phi, psi
+  bad = bad || f[10] < -he || f[10] > he;               // theta
+  bad = bad || f[14] < 0.0f;                            // goal z >= 0
+  return bad;  // NaN compares false: non-finite values never count
+}
+
 struct EnvArgs {
   int64_t n;
   int32_t K, down_sample, max_steps, flags;
@@ -511,7 +524,8 @@ struct StepArgs {
   int32_t* ep_len;
   int32_t* done_idx;
   int32_t* n_done;
-  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine count (handle-owned)
+  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine count (handle-owned); [2]:
+                                  // F16_FLAG_OBS_CHECK out-of-bounds lane-steps
   int32_t lds_image;
   // rollout slot (f16env_step_rollout; all NULL / 0 for f16env_step)
   int32_t sample_act;          // act == NULL: draw the actions in-kernel (seed, step)
@@ -624,6 +638,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   };
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = k < nE;
+  F16_CHECK(rows >= 0 && rows <= 64 && (!live || row0 + lane < nE), DBG_STATE_INDEX);
+  if (WIN) F16_CHECK(a.wpos >= a.E.K - 1 && a.wpos >= 0, DBG_WINDOW_POS);
   int done = 0;
   Lane L;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -750,12 +766,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       int base = 0;
       if (lane == 0) base = atomicAdd(a.n_done, __popcll(m));
       base = __shfl(base, 0);
+      F16_CHECK(base + __popcll(m) <= nE, DBG_DONE_LIST);
       if (done) a.done_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
     }
   }
   if (a.E.flags & F16_FLAG_NAN_GUARD) {
     const unsigned long long qm = __ballot(flags_out & 4);
     if (qm && lane == 0) atomicAdd(a.nonfinite, (unsigned long long)__popcll(qm));
+  }
+  if (a.E.flags & F16_FLAG_OBS_CHECK) {  // jsbsim_gym.py:268-285 on the new frame
+    const unsigned long long om = __ballot(live && obs_out_of_bounds(f));
+    if (om && lane == 0) atomicAdd(a.nonfinite + 2, (unsigned long long)__popcll(om));
   }
   if (live) {
     a.rew[k] = rew_out;
@@ -1156,6 +1177,7 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
     if (fl & 4) atomicAdd(a.nonfinite, 1ull);  // rare: one lane at a time
     const int64_t row = (int64_t)t * N + k;
     const int nslot = head == 0 ? K - 1 : head - 1;  // newest frame
+    F16_CHECK(head >= 0 && head < K && nslot >= 0 && nslot < K, DBG_RING_SLOT);
     if (coalesced) {
       __builtin_amdgcn_wave_barrier();
       const float* src = ring + nslot * slot_stride + (size_t)(wave * 64) * RING_PITCH;
@@ -1230,6 +1252,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
   if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // after the only barrier
   for (int64_t i = i0; i < nd; i += (int64_t)gridDim.x * BLOCK) {
     const int64_t k = i == i0 ? k0 : a.done_idx[i];
+    F16_CHECK(k >= 0 && k < a.E.n, DBG_RESET_INDEX);
     if (k < 0 || k >= a.E.n) continue;
     Lane L;
     lane_load<true>(a.s, k, L);
@@ -1313,6 +1336,7 @@ __global__ void f16_window_restart_kernel(int64_t n, int32_t K, int64_t wenv, in
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * per) return;
   const int64_t b = i >= per, t = i - b * per;
+  F16_CHECK(p_src >= 1, DBG_WINDOW_POS);
   float* h = b ? h1 : h0;
   if (wenv == 4 * 4 && wpos == n * 16) {  // position-major: the K-1 positions are one block
     float4* h4 = reinterpret_cast<float4*>(h);
@@ -1473,17 +1497,27 @@ __global__ __launch_bounds__(BLOCK) void f16_trim_kernel(int64_t n, const double
   const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (k >= n) return;
   const double* icb = ic_in + (int64_t)F16_IC_N * k;
+  // Newton on x = (alpha, elevator cmd, throttle cmd) as the oracle's trim_one, with what the
+  // fp32 residual needs to converge to its own noise floor (~1e-4 ft/s^2): central differences
+  // (the forward ones of the fp64 oracle carry an O(h) bias at the step size fp32 allows), up
+  // to 24 iterations, and the iterate with the smallest residual kept (fp32 noise can make the
+  // last step a slightly worse one)
   float x[3] = {0.05f, 0.0f, 0.5f};
-  const float hs[3] = {1e-3f, 1e-3f, 1e-3f};
-  float r[3];
-  for (int it = 0; it < 12; ++it) {
+  const float hs[3] = {2e-3f, 2e-3f, 2e-3f};
+  float r[3], best[3] = {x[0], x[1], x[2]}, best_r = 3.4e38f;
+  for (int it = 0;; ++it) {
     trim_residual(icb, x, sT, C, r);
+    const float rmax = fmaxf(fabsf(r[0]), fmaxf(fabsf(r[1]), fabsf(r[2])));
+    if (rmax < best_r) { best_r = rmax; best[0] = x[0]; best[1] = x[1]; best[2] = x[2]; }
+    if (rmax < 2e-5f || it == 24) break;
     float Jm[9], Ji[9];
     for (int j = 0; j < 3; ++j) {
-      float xp[3] = {x[0], x[1], x[2]}, rp[3];
+      float xp[3] = {x[0], x[1], x[2]}, xm[3] = {x[0], x[1], x[2]}, rp[3], rm[3];
       xp[j] += hs[j];
+      xm[j] -= hs[j];
       trim_residual(icb, xp, sT, C, rp);
-      for (int i = 0; i < 3; ++i) Jm[3 * i + j] = (rp[i] - r[i]) / hs[j];
+      trim_residual(icb, xm, sT, C, rm);
+      for (int i = 0; i < 3; ++i) Jm[3 * i + j] = (rp[i] - rm[i]) / (2.0f * hs[j]);
     }
     bool ok;
     inv3f(Jm, Ji, ok);
@@ -1495,6 +1529,7 @@ __global__ __launch_bounds__(BLOCK) void f16_trim_kernel(int64_t n, const double
     x[1] = clipf(x[1], -1.0f, 0.44f);
     x[2] = clipf(x[2], 0.0f, 1.0f);
   }
+  x[0] = best[0]; x[1] = best[1]; x[2] = best[2];
   trim_residual(icb, x, sT, C, r);
   double* o = ic_out + (int64_t)F16_IC_N * k;
   for (int j = 0; j < F16_IC_N; ++j) o[j] = icb[j];
@@ -1600,6 +1635,7 @@ __global__ __launch_bounds__(256) void f16_features_strided_kernel(int64_t n_row
   if (t < nf) {
     const int64_t i = f0 + t;
     const int64_t r = i / K, kk = i - r * K;
+    F16_CHECK(i < n_frames && r < n_rows && kk < K, DBG_FRAME_INDEX);
     const float* o = obs + r * row_stride + kk * frame_stride;
     float x[FEAT_IN];
     if ((frame_stride & 3) == 0 && (row_stride & 3) == 0 && ((uintptr_t)obs & 15) == 0) {  // 16-B aligned frames
@@ -1839,11 +1875,11 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   soa_carve(h->tmem, 1, h->tmpl);
   hipMemset(h->done_buf + cfg->n_envs, 0, 2 * sizeof(int32_t));
   h->done_par = 0;
-  if (hipMalloc((void**)&h->nonfinite, 2 * sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMalloc((void**)&h->nonfinite, 4 * sizeof(unsigned long long)) != hipSuccess) {
     hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); delete h;
     return set_err(-3, "hipMalloc(counter) failed");
   }
-  hipMemset(h->nonfinite, 0, sizeof(unsigned long long));
+  hipMemset(h->nonfinite, 0, 4 * sizeof(unsigned long long));
   {
     const int KC = cfg->stack_k * F16_OBS_DIM;
     const size_t img = sizeof(float) * (BLOCK / 64) * ((size_t)64 * KC + 16);
@@ -2249,6 +2285,31 @@ int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count) {
   if (!h || !count) return set_err(-1, "null argument");
   unsigned long long v = 0;
   HIPCHK(hipMemcpyAsync(&v, h->nonfinite, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  *count = (uint64_t)v;
+  return 0;
+}
+
+int f16env_debug_checks(f16env_t h, void* stream, uint32_t* violations) {
+  if (!h || !violations) return set_err(-1, "null argument");
+#ifdef F16_DEBUG_CHECKS
+  unsigned int v = 0;
+  HIPCHK(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_f16_violations), sizeof v, 0, hipMemcpyDeviceToHost,
+                                  (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  *violations = v;
+  return 1;
+#else
+  (void)stream;
+  *violations = 0;
+  return 0;
+#endif
+}
+
+int f16env_obs_bounds_count(f16env_t h, void* stream, uint64_t* count) {
+  if (!h || !count) return set_err(-1, "null argument");
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, h->nonfinite + 2, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   *count = (uint64_t)v;
   return 0;

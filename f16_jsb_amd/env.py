@@ -22,6 +22,7 @@ import numpy as np
 from . import spaces
 from ._lib import F16EnvError, check, lib
 from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
+                  F16_FLAG_OBS_CHECK,
                   F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
@@ -56,7 +57,8 @@ class F16Envs:
 
     def __init__(self, n_envs: int, stack_k: int = 10, device=None, seed: int = 0,
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
-                 autoreset: bool = True, ic=None, nan_guard: bool = False, obs_layout: str = "contiguous",
+                 autoreset: bool = True, ic=None, nan_guard: bool = False, obs_check: bool = False,
+                 obs_layout: str = "contiguous",
                  history: int = 0, window_order: str = "position", **cfg_kw):
         """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
@@ -81,7 +83,7 @@ class F16Envs:
         raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         self._raw_stream = raw if raw is not None else (lambda i: torch.cuda.current_stream(i).cuda_stream)
         flags = int(cfg_kw.pop("flags", 0)) | (0 if autoreset else F16_FLAG_NO_AUTORESET) \
-            | (F16_FLAG_NAN_GUARD if nan_guard else 0)
+            | (F16_FLAG_NAN_GUARD if nan_guard else 0) | (F16_FLAG_OBS_CHECK if obs_check else 0)
         self.cfg: EnvConfig = config_default(n_envs=n_envs, stack_k=stack_k, seed=seed, env_id_base=env_id_base,
                                              max_steps=max_steps, down_sample=down_sample, flags=flags, ic=ic,
                                              **cfg_kw)
@@ -401,6 +403,15 @@ class F16Envs:
         check(lib().f16env_nonfinite_count(self._h, self._stream(), ctypes.byref(c)), "f16env_nonfinite_count")
         return int(c.value)
 
+    @property
+    def obs_bounds_count(self) -> int:
+        """Lane-steps since creation whose new observation frame had a finite value outside the
+        observation space (obs_check=True; jsbsim_gym.py:268-285's warning, counted on the
+        device). Waits for the handle's stream."""
+        c = ctypes.c_uint64()
+        check(lib().f16env_obs_bounds_count(self._h, self._stream(), ctypes.byref(c)), "f16env_obs_bounds_count")
+        return int(c.value)
+
     def get_state(self):
         s = self.torch.zeros((self.n, F16C_N), dtype=self.torch.float64, device=self.device)
         check(lib().f16env_get_state(self._h, self._stream(), _ptr(s)), "f16env_get_state")
@@ -536,6 +547,96 @@ class _HostStaging:
                 e.ep_len.index_select(0, i).cpu().numpy())
 
 
+class _HostWindow:
+    """Numpy mode over a windowed handle (obs_layout="window", position-major): the host keeps
+    a pinned mirror of the device's two frame histories, [2][Th][N][16], and per step copies
+    only the step's new 64-B slot block of each (position p of both device histories: 2 x N x 64
+    B, contiguous) instead of the whole (N, K, 15) observation (N x K x 60 B: 39 MB per step at
+    65 536 envs, K = 10). The host then repeats what the windowed step kernel does to the
+    windows of reset lanes (f16env.hip WIN block): lanes reset by this step get K-1 copies of
+    their reset frame in the current history's window, lanes reset by the previous step get
+    the same fill from the other history (the kernel's FRESH fill). The observation returned is
+    a strided numpy view (N, K, 15) of the current host history's window (strides 64 B, N x 64 B,
+    4 B), valid until the step after next -- the device layout's guarantee, which SB3 needs
+    (it stores obs one step later, on_policy_algorithm.py:247-254); the terminal observation is
+    the other history's window, as on the device. The host ring has its own Th positions and
+    moves its last K-1 to the front when full."""
+
+    def __init__(self, envs: "F16Envs", th: int = 0):
+        t = envs.torch
+        self.t, self.envs = t, envs
+        n, k = envs.n, envs.k
+        self.Th = int(th) if th else max(128, 4 * k)
+        pin = envs.device.type == "cuda"
+        self.H = t.zeros((2, self.Th, n, 16), dtype=t.float32, pin_memory=pin)
+        self.Hn = self.H.numpy()
+        self.flags = t.empty(envs.step_flags.shape, dtype=t.uint8, pin_memory=pin)
+        self.act = t.empty((n, 4), dtype=t.float32, pin_memory=pin)
+        self.par = 0
+        self.q = k - 1
+        self.prev_reset = None
+        self.autoreset = not (int(envs.cfg.flags) & F16_FLAG_NO_AUTORESET)
+
+    actions_to_device = _HostStaging.actions_to_device
+
+    def _view(self, par: int) -> np.ndarray:
+        k, q = self.envs.k, self.q
+        return self.Hn[par, q - k + 1:q + 1, :, :F16_OBS_DIM].transpose(1, 0, 2)
+
+    def fetch(self, obs_dev, with_flags: bool = True):
+        e, k, n = self.envs, self.envs.k, self.envs.n
+        if not with_flags:  # after a reset: the whole current window, into both host histories
+            self.q, self.prev_reset = k - 1, None
+            w = obs_dev.transpose(0, 1)
+            for b in (0, 1):
+                self.H[b, :k, :, :F16_OBS_DIM].copy_(w, non_blocking=True)
+            if e.device.type == "cuda":
+                self.t.cuda.current_stream(e.device).synchronize()
+            return self._view(self.par), None, None, None
+        q = self.q + 1
+        if q >= self.Th:  # host restart: the last K-1 positions to the front of both histories
+            for b in (0, 1):
+                self.Hn[b, :k - 1] = self.Hn[b, q - k + 1:q]
+            q = k - 1
+        par = self.par ^ 1
+        cur, p = e._cur, e._p
+        self.H[par, q].copy_(e._hist[cur, p], non_blocking=True)
+        self.H[par ^ 1, q].copy_(e._hist[cur ^ 1, p], non_blocking=True)
+        self.flags.copy_(e.step_flags, non_blocking=True)
+        self.t.cuda.current_stream(e.device).synchronize()
+        f = self.flags.numpy()
+        rew, term, trunc = f[:4 * n].view(np.float32), f[4 * n:5 * n], f[5 * n:6 * n]
+        Hc = self.Hn[par]
+        if k > 1 and self.prev_reset is not None and self.prev_reset.size:  # the kernel's FRESH fill
+            idx = self.prev_reset
+            Hc[q - k + 1:q, idx] = self.Hn[par ^ 1, q - 1, idx][None]
+        self.prev_reset = None
+        if self.autoreset:
+            idx = np.flatnonzero(term | trunc)
+            if idx.size:
+                if k > 1:  # lanes reset by this step: K-1 copies of their reset frame
+                    Hc[q - k + 1:q, idx] = Hc[q, idx][None]
+                self.prev_reset = idx
+        self.q, self.par = q, par
+        return self._view(par), rew, term, trunc
+
+    def done_rows(self, idx: np.ndarray):
+        """terminal obs (the other host history's window), episode return / length."""
+        e, t = self.envs, self.t
+        tobs = np.ascontiguousarray(self._view(self.par ^ 1)[idx])
+        i = t.as_tensor(idx, dtype=t.int64).to(e.device, non_blocking=True)
+        return tobs, e.ep_return.index_select(0, i).cpu().numpy(), e.ep_len.index_select(0, i).cpu().numpy()
+
+
+def _staging(envs, copy_obs: bool = False):
+    """The numpy-mode staging for a handle: the host window mirror for position-major windowed
+    handles (only the new slots cross PCIe), else whole-observation copies."""
+    if getattr(envs, "window", False) and not getattr(envs, "_env_major", True) and hasattr(envs, "_hist") \
+            and not copy_obs:
+        return _HostWindow(envs)
+    return _HostStaging(envs)
+
+
 class F16VecEnv(*_bases(SB3VecEnv)):
     """Vectorised drop-in for ``DummyVecEnv([lambda: Monitor(gym.make("JSBSim-v0"))] * N)``.
 
@@ -547,9 +648,13 @@ class F16VecEnv(*_bases(SB3VecEnv)):
     stable_baselines3 is importable this class IS a ``VecEnv`` subclass, so
     ``BaseAlgorithm._wrap_env`` (base_class.py:215) takes it as-is.
 
-    Numpy mode (default, what SB3 consumes): one pinned-memory copy of obs and one of the
-    packed rewards/flags per step, one stream sync; infos of lanes that did not finish share one
-    read-only dict. The obs array returned stays valid for two further steps (see _HostStaging).
+    Numpy mode (default, what SB3 consumes): the handle steps in the windowed layout and the
+    host keeps a pinned mirror of its frame histories, so per step only the new frame slots
+    (2 x N x 64 B) and the packed rewards/flags cross PCIe, one stream sync (_HostWindow); the
+    obs returned is a strided (N, K, 15) numpy view of that mirror, valid until the step after
+    next (SB3 stores it one step later). ``copy_obs=True`` returns contiguous copies instead
+    (whole-observation D2H per step, _HostStaging), for consumers that keep observations
+    longer. Infos of lanes that did not finish share one read-only dict.
     ``return_numpy=False`` keeps everything on the GPU (infos is then None: the caller reads the
     ``last_step`` device tensors). ``envs=`` wraps an existing handle instead of creating one.
     The handle it creates steps in the windowed observation layout in numpy mode and in the
@@ -558,7 +663,7 @@ class F16VecEnv(*_bases(SB3VecEnv)):
     metadata = {"render_modes": []}
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
-                 return_numpy: bool = True, env_id_base: int = 0, envs=None, **kw):
+                 return_numpy: bool = True, env_id_base: int = 0, envs=None, copy_obs: bool = False, **kw):
         if envs is None:
             # numpy mode copies every observation to the host anyway, so the env steps in the
             # windowed layout (no per-step stack rewrite: 16.9 vs 27.8 us at K = 10, 65 536 envs);
@@ -579,7 +684,8 @@ class F16VecEnv(*_bases(SB3VecEnv)):
             self._seeds: list = [None for _ in range(n)]
             self._options: list = [{} for _ in range(n)]
         self.return_numpy = bool(return_numpy)
-        self._host = _HostStaging(self.envs) if self.return_numpy else None
+        self.copy_obs = bool(copy_obs)
+        self._host = _staging(self.envs, self.copy_obs) if self.return_numpy else None
         self._actions = None
         self._t_start = time.time()
         self.last_step: Optional[StepOut] = None
@@ -627,6 +733,8 @@ class F16VecEnv(*_bases(SB3VecEnv)):
                 if term_u8[i] & 2:  # NaN guard quarantine (nan_guard=True)
                     info["nonfinite"] = True
                 infos[i] = info
+        if self.copy_obs:
+            obs = np.array(obs)
         return obs, rew.copy(), dones, infos
 
     def step(self, actions):
@@ -697,7 +805,10 @@ class F16VecEnv(*_bases(SB3VecEnv)):
         if method_name == "reset":
             mask = np.zeros(self.num_envs, np.uint8)
             mask[idx] = 1
-            obs = self.envs.reset(mask=mask)[self.envs.torch.as_tensor(idx, device=self.envs.device)]
+            full = self.envs.reset(mask=mask)
+            if self._host is not None:  # the host mirror takes the new windows
+                self._host.fetch(full, with_flags=False)
+            obs = full[self.envs.torch.as_tensor(idx, device=self.envs.device)]
             return [(o, {}) for o in obs.cpu().numpy()]
         raise AttributeError("F16VecEnv lanes have no per-env method %r" % method_name)
 
@@ -757,7 +868,7 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
         self.spec = None
         self.closed = False
         self.return_numpy = bool(return_numpy)
-        self._host = _HostStaging(self.envs) if self.return_numpy else None
+        self._host = _staging(self.envs) if self.return_numpy else None
         self._t_start = time.time()
 
     def reset(self, *, seed=None, options=None):

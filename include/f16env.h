@@ -138,6 +138,12 @@ enum f16_latch_index {
  * reward 0 and terminated[i] = 3 (bit 1 marks the quarantine), is auto-reset like any finished
  * lane, and is counted (f16env_nonfinite_count). Off by default. */
 #define F16_FLAG_NAN_GUARD 0x8
+/* Observation-bounds diagnostic (jsbsim_gym.py:268-285: observation_space.contains(obs) and
+ * the warning for FINITE values outside SINGLE_OBS_LOW / SINGLE_OBS_HIGH, :28-53): each step
+ * checks the lane's new frame (the older K-1 frames were checked when they were new) and counts
+ * the lanes with a finite component out of bounds (f16env_obs_bounds_count). Off by default;
+ * changes nothing else. */
+#define F16_FLAG_OBS_CHECK 0x10
 
 typedef struct f16env_config {
   int32_t n_envs;       /* envs on this device                                          */
@@ -295,6 +301,14 @@ int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step
 
 /* Lanes quarantined by F16_FLAG_NAN_GUARD since create (waits for `stream`). */
 int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);
+/* Debug build (libf16env_debug.so, compiled with F16_DEBUG_CHECKS): the bits of
+ * the index / range invariants the kernels found violated since the library was loaded
+ * (f16_device.h DebugBits; waits for `stream`). Returns 1 in the debug build, 0 (and
+ * *violations = 0) in the product build, which carries no checks. */
+int f16env_debug_checks(f16env_t h, void* stream, uint32_t* violations);
+/* Lane-steps whose new observation frame had a finite value outside the observation space
+ * since create (F16_FLAG_OBS_CHECK; waits for `stream`). */
+int f16env_obs_bounds_count(f16env_t h, void* stream, uint64_t* count);
 
 /* Canonical state export/import: canon is N x F16C_N double (device). The latch's p/q/r-aero
  * and ground speed are recomputed from the state on import (they are functions of it);

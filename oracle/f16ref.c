@@ -425,7 +425,21 @@ struct f16ref {
   int n;
   env_t* env;
   float* stacks;
+  uint64_t obs_oob; /* F16_FLAG_OBS_CHECK: lane-steps with a finite out-of-bounds new frame */
 };
+
+/* jsbsim_gym.py:268-285: observation_space.contains(obs) fails on a FINITE value outside
+ * SINGLE_OBS_LOW / SINGLE_OBS_HIGH (:28-53, float32 arrays); checked on the new frame */
+static int obs_out_of_bounds(const float* f) {
+  static const float pe = (float)(3.14159265358979323846 + 1e-5), he = (float)(1.5707963267948966 + 1e-5);
+  const float lo[F16_OBS_DIM] = {-INFINITY, -INFINITY, -INFINITY, 0.0f, -pe, -pe, -INFINITY, -INFINITY, -INFINITY,
+                                 -pe, -he, -pe, -INFINITY, -INFINITY, 0.0f};
+  const float hi[F16_OBS_DIM] = {INFINITY, INFINITY, INFINITY, INFINITY, pe, pe, INFINITY, INFINITY, INFINITY,
+                                 pe, he, pe, INFINITY, INFINITY, INFINITY};
+  for (int j = 0; j < F16_OBS_DIM; j++)
+    if (isfinite(f[j]) && (f[j] < lo[j] || f[j] > hi[j])) return 1;
+  return 0;
+}
 
 static void derive(const env_t* e, derived_t* d) {
   /* Ti2ec (FGLocation) and vLocation = Ti2ec * vInertialPosition */
@@ -1021,6 +1035,7 @@ void f16ref_destroy(f16ref* h) {
   free(h->env); free(h->stacks); free(h);
 }
 int f16ref_n_envs(const f16ref* h) { return h->n; }
+uint64_t f16ref_obs_bounds_count(const f16ref* h) { return h->obs_oob; }
 int f16ref_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();
@@ -1081,6 +1096,10 @@ int f16ref_step(f16ref* h, const float* act, float* obs, float* rew, uint8_t* te
     int bad = 0;
     if (h->cfg.flags & F16_FLAG_NAN_GUARD)
       for (int j = 0; j < 9; j++) bad |= !isfinite(f[j]);
+    if ((h->cfg.flags & F16_FLAG_OBS_CHECK) && obs_out_of_bounds(f)) {
+#pragma omp atomic
+      h->obs_oob++;
+    }
     double r = 0.0;
     int te = 0, tr = 0;
     if (bad) {

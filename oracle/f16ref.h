@@ -72,6 +72,7 @@ double f16ref_seek(double v, double target, double accel, double decel, double d
 /* Number of OpenMP threads the batch loops use (1 if built without OpenMP). */
 int f16ref_threads(void);
 int f16ref_set_threads(int n);
+uint64_t f16ref_obs_bounds_count(const f16ref* h);
 
 #ifdef __cplusplus
 }

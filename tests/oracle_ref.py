@@ -14,7 +14,8 @@ import numpy as np
 from f16_jsb_amd.abi import (F16C_N, F16_IC_N, F16_OBS_DIM, EnvConfig, config_default)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "oracle", "_build", "libf16ref.so")
+# F16REF_LIB: another build of the oracle, e.g. the ASan/UBSan one (oracle/Makefile `sanitize`)
+LIB_PATH = os.environ.get("F16REF_LIB") or os.path.join(ROOT, "oracle", "_build", "libf16ref.so")
 
 _lib = None
 
@@ -53,6 +54,8 @@ def lib():
         L.f16ref_n_aero_fns.restype = i32
         L.f16ref_threads.restype = i32
         L.f16ref_set_threads.argtypes = [i32]
+        L.f16ref_obs_bounds_count.argtypes = [vp]
+        L.f16ref_obs_bounds_count.restype = u64
         L.f16ref_set_threads.restype = i32
         L.f16ref_set_physics_mask.argtypes = [i32]
         L.f16ref_get_physics_mask.restype = i32
@@ -129,6 +132,10 @@ class OracleEnvs:
         res = np.zeros((self.n, 3), np.float64)
         lib().f16ref_trim(self._h, _p(ic), _p(out), _p(res))
         return out, res
+
+    @property
+    def obs_bounds_count(self):
+        return int(lib().f16ref_obs_bounds_count(self._h))
 
     def sample_actions(self, seed, step):
         a = np.zeros((self.n, 4), np.float32)

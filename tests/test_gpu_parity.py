@@ -383,6 +383,45 @@ def test_vecenv_sb3_contract(torch_mod):
     env.close()
 
 
+@pytest.mark.parametrize("k,cfg5", [(4, False), (10, False), (4, True)])
+def test_vecenv_host_window_matches_full_copy(torch_mod, k, cfg5):
+    """F16VecEnv numpy mode with the host window mirror (_HostWindow: only the step's new frame
+    slots cross PCIe, the host repeats the kernel's reset-window fills) against whole-observation
+    copies (copy_obs=True) on identical handles: observations, rewards, dones, terminal
+    observations and episode statistics bit-identical at every step, through short episodes
+    (auto-resets every few steps, cfg5's in-step resets), device window restarts (history 16)
+    and host ring restarts (Th = 2K + 3); the obs returned one step earlier is unchanged."""
+    from f16_jsb_amd.env import F16VecEnv, _HostStaging, _HostWindow
+    n = 700
+    kw = dict(num_envs=n, stack_k=k, seed=3, max_steps=7, history=max(16, 2 * k), cfg5=cfg5)
+    a = F16VecEnv(**kw)
+    a._host = _HostWindow(a.envs, th=2 * k + 3)
+    b = F16VecEnv(copy_obs=True, **kw)
+    assert isinstance(b._host, _HostStaging) and not isinstance(b._host, _HostWindow)
+    np.testing.assert_array_equal(a.reset(), b.reset())
+    rng = np.random.default_rng(1)
+    prev = None
+    ended = 0
+    for t in range(60):
+        act = rng.uniform([-1, -1, -1, 0], [1, 1, 1, 1], (n, 4)).astype(np.float32)
+        oa, ra, da, ia = a.step(act)
+        ob, rb, db, ib = b.step(act)
+        np.testing.assert_array_equal(oa, ob, err_msg="obs @%d" % t)
+        np.testing.assert_array_equal(ra, rb)
+        np.testing.assert_array_equal(da, db)
+        for i in np.flatnonzero(db):
+            np.testing.assert_array_equal(ia[i]["terminal_observation"], ib[i]["terminal_observation"])
+            assert ia[i]["episode"]["r"] == ib[i]["episode"]["r"] and ia[i]["episode"]["l"] == ib[i]["episode"]["l"]
+            assert ia[i]["TimeLimit.truncated"] == ib[i]["TimeLimit.truncated"]
+            ended += 1
+        if prev is not None:
+            np.testing.assert_array_equal(prev[0], prev[1], err_msg="previous obs changed @%d" % t)
+        prev = (oa, oa.copy())
+    assert ended > n
+    a.close()
+    b.close()
+
+
 def test_global_table_variant_bit_identical(torch_mod, monkeypatch):
     """The global-table step kernel (chosen when the K-frame stack image fills LDS, e.g. the
     reference's K = 10) runs the same arithmetic as the LDS-table kernel: forced on a K = 4
@@ -446,6 +485,55 @@ def test_cfg2_trimmed_level_flight_4096(torch_mod):
             tol = TOL_STEP * 4 if t <= 10 else (TOL_CONST300 if t == 100 else tol_long)
             _assert_frames(out.obs.cpu().numpy()[live, -1], o_r[live, -1], tol, "cfg2 trimmed @%d" % t)
     assert np.median(np.abs(o_r[ok, -1, 2] - h0[ok])) < 30.0
+
+
+def test_cfg2_device_trim_grid_4096(torch_mod):
+    """BASELINE cfg2 as bench.py runs it: the DEVICE trim (f16_trim_kernel, fp32 Newton) of the
+    64 x 64 altitude x airspeed grid against the oracle's fp64 trim of the same grid: wherever
+    the oracle converges (residual < 1e-3), the device trim converges too (residual < 1e-3) to
+    the same (alpha, elevator, throttle); then the device-trimmed ICs are flown 1 199 steps on
+    both paths with their constant trim action (the reference never trims: jsbsim_gym.py:
+    166-170), per state at steps {1, 10, 100, 1199} as test_cfg2_trimmed_level_flight_4096."""
+    torch = torch_mod
+    n = 4096
+    ic = np.tile(default_ic(), (n, 1))
+    hh, uu = np.meshgrid(np.linspace(3000, 30000, 64), np.linspace(600, 1200, 64), indexing="ij")
+    ic[:, 2], ic[:, 3] = hh.ravel(), uu.ravel()
+    ref, g = _pair(n, 4, seed=3)
+    t_r, res_r = ref.trim(ic)
+    t_g, res_g = g.trim(ic)
+    t_g, res_g = t_g.cpu().numpy(), res_g.cpu().numpy()
+    ok_r = res_r.max(axis=1) < 1e-3
+    ok_g = res_g.max(axis=1) < 1e-3
+    print("cfg2 grid: oracle trimmed %.4f, device trimmed %.4f, device residual on the oracle's set: max %.2e "
+          "p99 %.2e; |d alpha| max %.2e, |d ele| %.2e, |d thr| %.2e" % (
+              ok_r.mean(), ok_g.mean(), res_g[ok_r].max(), np.percentile(res_g[ok_r].max(axis=1), 99),
+              np.abs(t_g[ok_r, 7] - t_r[ok_r, 7]).max(), np.abs(t_g[ok_r, 13] - t_r[ok_r, 13]).max(),
+              np.abs(t_g[ok_r, 15] - t_r[ok_r, 15]).max()))
+    assert ok_r.mean() > 0.95, ok_r.mean()
+    assert ok_g[ok_r].all(), "device trim residual >= 1e-3 where the oracle converged: %s" % res_g[ok_r & ~ok_g][:4]
+    np.testing.assert_allclose(t_g[ok_r, 7], t_r[ok_r, 7], atol=2e-4)    # alpha = theta
+    np.testing.assert_allclose(t_g[ok_r, 13], t_r[ok_r, 13], atol=2e-3)  # elevator cmd
+    np.testing.assert_allclose(t_g[ok_r, 15], t_r[ok_r, 15], atol=2e-3)  # throttle cmd
+    goals = np.zeros((n, 3), np.float32)
+    goals[:, 2] = 50000.0
+    o_r = ref.reset(goals=goals, ic=t_g)
+    g.reset(goals=goals, ic=t_g)
+    act = np.zeros((n, 4), np.float32)
+    act[:, 1], act[:, 3] = t_g[:, 13], t_g[:, 15]
+    ta = torch.as_tensor(act).cuda()
+    h0 = o_r[:, 0, 2].copy()
+    tol_long = np.array([3.0, 3.0, 3.0, 3e-4, 5e-5, 1e-5, 5e-5, 5e-5, 1e-5, 2e-4, 6e-4, 5e-5, 0, 0, 0])
+    for t in range(1, 1200):
+        o_r, r_r, te_r, tr_r, *_ = ref.step(act)
+        out = g.step(ta)
+        if t in (1, 10, 100, 1199):
+            te_g = out.terminated.cpu().numpy().astype(bool)
+            np.testing.assert_array_equal(te_g, te_r)
+            live = ok_r & ~te_r
+            tol = TOL_STEP * 4 if t <= 10 else (TOL_CONST300 if t == 100 else tol_long)
+            _assert_frames(out.obs.cpu().numpy()[live, -1], o_r[live, -1], tol, "cfg2 device trim @%d" % t)
+    assert np.median(np.abs(o_r[ok_r, -1, 2] - h0[ok_r])) < 30.0
 
 
 def test_gymnasium_vector_env_contract(torch_mod):
@@ -528,6 +616,47 @@ def test_nan_guard_quarantines_nonfinite_lanes(torch_mod):
     assert not bool(torch.isfinite(ob.obs[bad]).all())
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "window"])
+def test_obs_bounds_diagnostic_counts_like_oracle(torch_mod, layout):
+    """F16_FLAG_OBS_CHECK: the device counterpart of jsbsim_gym.py:268-285 (a FINITE value
+    outside the observation space, SINGLE_OBS_LOW / HIGH :28-53). Lanes given a goal below
+    ground (goal z < 0 through set_state) put a finite out-of-bounds value into every new frame;
+    the device count of such lane-steps equals the oracle's, the physics is unchanged (same
+    frames as a handle without the check), and in-bounds flight counts nothing."""
+    torch = torch_mod
+    from f16_jsb_amd.abi import F16_FLAG_OBS_CHECK, F16C_GOAL
+    from f16_jsb_amd.env import F16Envs
+    n, steps = 512, 20
+    ref = OracleEnvs(n, stack_k=4, seed=9, flags=F16_FLAG_OBS_CHECK)
+    g = F16Envs(n, stack_k=4, seed=9, obs_check=True, obs_layout=layout)
+    plain = F16Envs(n, stack_k=4, seed=9, obs_layout=layout)
+    o = ref.reset()
+    g.reset()
+    plain.reset()
+    for t in range(1, 4):  # in bounds: nothing counted
+        a = ref.sample_actions(2, t)
+        ref.step(a)
+        g.step(torch.as_tensor(a).cuda())
+        plain.step(torch.as_tensor(a).cuda())
+    assert g.obs_bounds_count == 0 and ref.obs_bounds_count == 0
+    s = ref.get_state()
+    bad = np.arange(n) % 7 == 0
+    s[bad, F16C_GOAL + 2] = -100.0
+    ref.set_state(s)
+    for h in (g, plain):
+        h.set_state(s)
+    for t in range(4, 4 + steps):
+        a = ref.sample_actions(2, t)
+        ref.step(a)
+        og = g.step(torch.as_tensor(a).cuda())
+        op = plain.step(torch.as_tensor(a).cuda())
+        assert torch.equal(og.obs, op.obs) and torch.equal(og.rew, op.rew)
+    assert ref.obs_bounds_count == int(bad.sum()) * steps
+    assert g.obs_bounds_count == ref.obs_bounds_count
+    for h in (ref, g, plain):
+        h.close()
 
 
 def test_host_checks_refuse_misshaped_buffers(torch_mod):

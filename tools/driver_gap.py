@@ -17,6 +17,7 @@ timed region several ways:
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -77,6 +78,13 @@ def main():
         elif preface == "torch_op":  # a small torch launch + sync first
             torch.zeros(1, device=dev).add_(1)
             torch.cuda.synchronize()
+        elif preface == "gc":  # bench.py r03b: gc.collect() right before the region
+            gc.collect()
+        elif preface == "noop":  # one tiny launch after the sync, before t0 (host launch path warm)
+            noop()
+        elif preface == "gc_noop":
+            gc.collect()
+            noop()
         hs = []
         t0 = time.perf_counter()
         if pre_spin_cycles:
@@ -91,14 +99,30 @@ def main():
         host = np.diff(np.array([t0] + hs)) * 1e6
         return s.elapsed_time(en) * 1e3 / K, wall * 1e6 / K, host
 
+    # the launch call alone inside step(): its host time on the region's first call
+    real_bound = e._step_bound
+    launch_us = []
+
+    def timed_bound(*a):
+        tb = time.perf_counter()
+        r = real_bound(*a)
+        launch_us.append((time.perf_counter() - tb) * 1e6)
+        return r
+    e._step_bound = timed_bound
+    zero = torch.zeros(1, device=dev)
+
+    def noop():
+        zero.add_(0)
     variants = {}
-    for pre in ("plain", "bench", "bench_spin", "torch_op", "bench"):
+    for pre in ("plain", "bench", "gc", "noop", "gc_noop", "bench_spin", "torch_op", "plain"):
         rs = []
         for tr in range(3):
+            launch_us.clear()
             r_us, wall_us, host = region(preface=pre)
-            rs.append((round(r_us, 3), round(wall_us, 3), round(float(host[0]), 2)))
+            rs.append((round(r_us, 3), round(wall_us, 3), round(float(host[0]), 2), round(launch_us[0], 2)))
         variants.setdefault(pre, []).extend(rs)
-        print(pre, rs, flush=True)
+        print(pre, "(region us/step, wall us/step, first call us, its launch us)", rs, flush=True)
+    e._step_bound = real_bound
     res["preface_variants"] = variants
     for tr in range(args.trials):
         r_us, wall_us, host = region()
