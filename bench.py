@@ -432,6 +432,32 @@ def sb3_compat_bench(dev, n, steps=20):
                     "PCIe-inclusive: pinned staging, one obs + one packed flag copy, shared info for running lanes)"}
 
 
+def cfg1_hip_bench(dev, steps=1000):
+    """BASELINE cfg1 on the HIP path: ONE env, K = 10, 1 000 random-action steps (numpy
+    default_rng(0) actions, uploaded once), the per-step latency of a single-env step launch
+    through F16Envs.step -- the GPU is the wrong tool for one env; reported beside the CPU
+    oracle's cfg1 figure (cpu_baseline.cfg1)."""
+    import numpy as np
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    e = F16Envs(1, stack_k=10, device=dev, seed=0)
+    e.reset()
+    acts = torch.as_tensor(np.random.default_rng(0).uniform([-1, -1, -1, 0], [1, 1, 1, 1], (steps, 1, 4))
+                           .astype(np.float32), device=dev)
+    for t in range(20):
+        e.step(acts[t])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        e.step(acts[t])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    name = e.step_kernel_name
+    e.close()
+    return {"envs": 1, "stack_k": 10, "steps": steps, "kernel": name, "ms_per_step": round(el / steps * 1e3, 5),
+            "env_steps_per_s": round(steps / el, 1)}
+
+
 def layout_leg(dev, args, layout, steps=300):
     """The headline workload in the other observation layout, beside the headline (N=1): same
     phase spread + burn-in, `steps` timed steps (region HIP events) and the kernel's own
@@ -594,7 +620,11 @@ def main():
     layouts = layout_leg(dev, args, other) if (world == 1 and not cfg5) else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
-        rollout = rollout_bench(args, dev, rank, world)
+        try:  # a side leg: its failure (e.g. a collective error at N > 1) must not lose the headline
+            rollout = rollout_bench(args, dev, rank, world)
+        except Exception as ex:  # noqa: BLE001
+            rollout = {"error": "%s: %s" % (type(ex).__name__, ex)}
+    cfg1 = cfg1_hip_bench(dev) if (world == 1 and not cfg5) else None
 
     if rank != 0:
         dist.destroy_process_group()
@@ -653,11 +683,13 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
             "valu": None if cfg5 else load_valu(n, args.stack, kernel_name),
-            "kernel": kernel_name + (" + f16_reset_done_kernel" if cfg5 else ""),
+            # cfg5: auto-resets happen inside the step kernel from the reset cache, which
+            # f16_ic_fill_kernel refills every F16ENV_ICC_PERIOD (32) steps
+            "kernel": kernel_name + (" + f16_ic_fill_kernel (reset cache refill)" if cfg5 else ""),
             "waves_per_simd": waves_per_simd,
             "kernel_ms": round(roof_ms, 5),
             "kernel_ms_min": round(kern_min_ms, 5),
-            "kernel_timing": ("HIP events around the timed region / launches (step + reset kernels)" if cfg5 else
+            "kernel_timing": ("HIP events around the timed region / launches (step kernels + the amortised reset-cache refills)" if cfg5 else
                               "start/stop HIP events recorded by each launch's dispatch packet (hipExtLaunchKernel) "
                               "on the launch stream, mean over %d launches" % nk),
             "region_ms_per_launch": round(gpu_ms_per_step, 5),
@@ -689,6 +721,8 @@ def main():
         out["cfg2"] = cfg2
     if persist is not None:
         out["persistent_random_policy"] = persist
+    if cfg1 is not None:
+        out["cfg1_hip"] = cfg1
     if layouts is not None:
         out["layouts"] = {args.obs_layout: {"kernel": kernel_name, "kernel_ms": round(kern_ms, 5),
                                             "region_ms_per_step": round(gpu_ms_per_step, 5)},

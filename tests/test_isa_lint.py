@@ -5,9 +5,16 @@ carried a run-time reset path. Round 3 found the cause in the ISA: the shaping t
 r += 0.01 (last_d - d) of PositionReward (jsbsim_gym.py:493-507) compiled to
 `v_sub_f32 v0, v207, v207` -- the register allocator wrote the new distance into the tuple
 register that still held the previous one before reading it (a backend miscompile of ROCm 7.2's
-LLVM; the source workaround is in env_reward, f16env.hip). No source expression of the library
-subtracts a value from itself, so any `v_sub_f32 vX, vY, vY` in the code object is that bug
-again; the test disassembles every kernel and fails on one.
+LLVM; the source workaround is in env_reward, f16env.hip). No fp32 source expression of the
+library subtracts a value from itself, so any `v_sub_f32 vX, vY, vY` (or `v_add_f32 vX, vY, -vY`)
+in the code object is that bug again; the test disassembles every kernel and fails on one.
+
+fp64 `v_add_f64 D, X, -X` does occur legitimately: derive() (f16_device.h) forms
+(float)(xE - A.r0[0]) etc. for the altitude advance, and where derive runs at the AltRef's own
+reference point (frame 0 of a step, every RunIC pass) both operands are the same value. The
+compiler keeps x - x (it is NaN, not 0, for non-finite x), and each such difference is narrowed
+by the (float) cast right after. The second test pins that shape: an fp64 self-difference whose
+result is not narrowed to fp32 within a few instructions is not derive's and fails.
 """
 from __future__ import annotations
 
@@ -47,8 +54,28 @@ def test_no_self_subtraction_in_step_kernels():
         if m:
             kernel = m.group(1)
             continue
-        if re.search(r"\bv_sub_f32(_e32|_e64)?\s+v\d+, (v\d+), \2(\s|$)", line):
+        if (re.search(r"\bv_sub(rev)?_f32(_e32|_e64)?\s+v\d+, (v\d+), \3(\s|$)", line)
+                or re.search(r"\bv_add_f32(_e32|_e64)?\s+v\d+, (v\d+), -\2(\s|$)", line)
+                or re.search(r"\bv_add_f32(_e32|_e64)?\s+v\d+, -(v\d+), \2(\s|$)", line)):
             bad.append((kernel, line.strip()))
     assert not bad, "x - x subtraction(s) in the code object (register-allocation miscompile): %s" % bad[:4]
     # the step kernels are in there at all (the scan saw the real code)
     assert "f16_step_win_nt_kernel" in asm and "f16_step_kernel" in asm
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="ROCm llvm-objdump not present")
+def test_fp64_self_differences_are_derive_reference_point():
+    from f16_jsb_amd.build import build
+    lines = _disassemble(build()).splitlines()
+    pat = re.compile(r"\bv_add_f64(_e64)?\s+(v\[\d+:\d+\]), (-?)(v\[\d+:\d+\]), (-?)(v\[\d+:\d+\])")
+    seen, bad = 0, []
+    for i, line in enumerate(lines):
+        m = pat.search(line)
+        if not m or m.group(4) != m.group(6) or m.group(3) == m.group(5):
+            continue
+        seen += 1
+        cvt = re.compile(r"\bv_cvt_f32_f64(_e32|_e64)?\s+v\d+, " + re.escape(m.group(2)) + r"(\s|$)")
+        if not any(cvt.search(nxt) for nxt in lines[i + 1:i + 40]):
+            bad.append(line.strip())
+    assert not bad, "fp64 x - x not narrowed to fp32 (not derive's reference-point difference): %s" % bad[:4]
+    assert seen > 0  # the pattern matches the disassembler's syntax (derive's are in there)

@@ -56,6 +56,9 @@ for s in $STEPS; do
         python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5) || exit $? ;;
     gap) run driver_gap_$TAG 300 python tools/driver_gap.py --json "$OUT/driver_gap_$TAG.json" ;;
     probe) run cp_pingpong_$TAG 120 tools/probes/cp_pingpong 2000 ;;
+    jsbsim)  # is a JSBSim binding present on the box? (probe only; never installed)
+      python -c "import jsbsim, sys; print('jsbsim', jsbsim.__version__)" > "$OUT/jsbsim_probe_$TAG.log" 2>&1
+      echo "[session] jsbsim probe rc=$?"; tail -2 "$OUT/jsbsim_probe_$TAG.log" ;;
     stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
     bench5) run bench_cfg5_$TAG 600 python bench.py --workload cfg5 --steps 300 --warmup 20 --cpu-seconds 5 ;;
     variants) run variant_sweep 900 python tools/variant_sweep.py run --json "$OUT/variants_$TAG.json" ;;
