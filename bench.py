@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1 process group: nccl (RCCL over xGMI, the measurement); gloo only "
+                         "rehearses the multi-rank code path on a box with fewer GPUs than ranks")
     ap.add_argument("--action-pool", type=int, default=0,
                     help="distinct pre-generated action batches (0 = one per timed step)")
     ap.add_argument("--rollout-envs", type=int, default=32768, help="cfg4 rollout envs per GPU (0 = skip)")
@@ -528,9 +531,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        # rehearsal only: ranks share the box's GPUs round-robin (device_count does not
+        # initialise the GPU); the nccl measurement keeps one GPU per rank
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -670,6 +680,8 @@ def main():
             "stack_k": args.stack,
             "fdm_frames_per_step": 4,
             "parallelism": "env-sharded x%d (no collective in the step loop)" % world,
+            **({"process_group": args.dist_backend + (" (rehearsal: ranks share GPUs)" if args.dist_backend == "gloo" else "")}
+               if world > 1 else {}),
         },
         "roofline": {
             # the path has no dense contraction, so the roof the fraction is quoted against is HBM

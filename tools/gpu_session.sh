@@ -54,6 +54,9 @@ for s in $STEPS; do
     profdrv)  # rocprofv3 summary of the driver's exact command
       (cd /tmp && run_abs prof_drv_$TAG 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/prof_drv_$TAG" -o run --output-format csv -- \
         python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5) || exit $? ;;
+    dist2)  # the bench's N > 1 code path with 2 ranks sharing this box's GPU (gloo: rehearsal only)
+      run bench_dist2_$TAG 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
     gap) run driver_gap_$TAG 300 python tools/driver_gap.py --json "$OUT/driver_gap_$TAG.json" ;;
     probe) run cp_pingpong_$TAG 120 tools/probes/cp_pingpong 2000 ;;
     jsbsim)  # is a JSBSim binding present on the box? (probe only; never installed)
