@@ -256,8 +256,9 @@ def rollout_bench(args, dev, rank, world):
         "gather_s": round(float(tt[2]), 4) if world > 1 else None,
         "gather_bytes_at_rank0": gathered if world > 1 else None,
         "gather_GBps_at_rank0": round(gathered / float(tt[2]) / 1e9, 2) if world > 1 and tt[2] > 0 else None,
-        "gather": "RCCL dist.gather, %d-step chunks, frame-deduplicated obs (newest frame + initial stack)"
-                  % args.gather_chunk if world > 1 else "n/a (1 GPU)",
+        "gather": "%s dist.gather, %d-step chunks, frame-deduplicated obs (newest frame + initial stack)"
+                  % ("RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)", args.gather_chunk)
+                  if world > 1 else "n/a (1 GPU)",
     }
     return r
 
