@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1199)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--obs-layout", default="window", choices=("window", "contiguous"),
+                    help="the GPU handle's layout (window: the bench's cfg5 kernels)")
     args = ap.parse_args()
     import torch
     from f16_jsb_amd.build import build
@@ -46,7 +48,7 @@ def main():
     n, K = args.n, 4
     kw = dict(stack_k=K, seed=args.seed, cfg5=True, flags=F16_FLAG_NO_AUTORESET)
     ref = OracleEnvs(n, **kw)
-    g = F16Envs(n, **kw)
+    g = F16Envs(n, obs_layout=args.obs_layout, **kw)
     o_r = ref.reset()
     o_g = g.reset().cpu().numpy()
     alive = np.ones(n, bool)
@@ -79,6 +81,7 @@ def main():
                 t, alive.sum(), rows[-1]["h_m:p99"] if rows else -1, rows[-1]["alpha:p99"] if rows else -1,
                 time.time() - t0), flush=True)
     res = {"n_envs": n, "stack_k": K, "seed": args.seed, "steps": args.steps,
+           "obs_layout": args.obs_layout, "kernel": g.step_kernel_name,
            "model": "cfg5: random IC box + Gauss-Markov gusts (include/f16env.h), random actions (Philox)",
            "done_flag_mismatches_while_alive": done_mismatch, "horizons": rows}
     if args.json:

@@ -65,7 +65,7 @@ for s in $STEPS; do
     stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
     bench5) run bench_cfg5_$TAG 600 python bench.py --workload cfg5 --steps 300 --warmup 20 --cpu-seconds 5 ;;
     variants) run variant_sweep 900 python tools/variant_sweep.py run --json "$OUT/variants_$TAG.json" ;;
-    div) run cfg5_divergence 900 python tests/cfg5_divergence.py --n 4096 --json "$OUT/cfg5_divergence_$TAG.json" ;;
+    div) run cfg5_divergence_$TAG 900 python tests/cfg5_divergence.py --n 4096 --json "$OUT/cfg5_divergence_$TAG.json" ;;
     sweep) run kernel_sweep 600 python tools/kernel_sweep.py --json "$OUT/sweep_$TAG.json" ;;
     report) run parity_report 600 python tests/parity_report.py --n 256 --steps 300 --json "$OUT/parity_$TAG.json" ;;
     prof)
