@@ -52,7 +52,8 @@ def main():
     o_r = ref.reset()
     o_g = g.reset().cpu().numpy()
     alive = np.ones(n, bool)
-    done_mismatch = 0
+    done_mismatch = 0  # read by record() at each horizon
+    first_mismatch = None
     rows = []
     t0 = time.time()
 
@@ -61,7 +62,7 @@ def main():
             return
         e = frame_err(o_g[alive, -1], o_r[alive, -1])[:, :12]
         pct = np.percentile(e, [50, 90, 99, 100], axis=0)
-        rows.append({"step": t, "alive": int(alive.sum()),
+        rows.append({"step": t, "alive": int(alive.sum()), "done_mismatches_so_far": done_mismatch,
                      **{"%s:p%s" % (FRAME_NAMES[c], q): float(pct[i, c])
                         for c in range(12) for i, q in enumerate(("50", "90", "99", "max"))}})
 
@@ -73,7 +74,10 @@ def main():
         o_g = out.obs.cpu().numpy()
         d_g = (out.terminated | out.truncated).cpu().numpy().astype(bool)
         d_r = te_r | tr_r
-        done_mismatch += int((alive & (d_g != d_r)).sum())
+        mm = int((alive & (d_g != d_r)).sum())
+        if mm and first_mismatch is None:
+            first_mismatch = t
+        done_mismatch += mm
         alive &= ~(d_g | d_r)
         if t in HORIZONS:
             record(t)
@@ -83,7 +87,8 @@ def main():
     res = {"n_envs": n, "stack_k": K, "seed": args.seed, "steps": args.steps,
            "obs_layout": args.obs_layout, "kernel": g.step_kernel_name,
            "model": "cfg5: random IC box + Gauss-Markov gusts (include/f16env.h), random actions (Philox)",
-           "done_flag_mismatches_while_alive": done_mismatch, "horizons": rows}
+           "done_flag_mismatches_while_alive": done_mismatch, "first_done_mismatch_step": first_mismatch,
+           "horizons": rows}
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
