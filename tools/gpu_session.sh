@@ -59,6 +59,7 @@ for s in $STEPS; do
         --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
     gap) run driver_gap_$TAG 300 python tools/driver_gap.py --json "$OUT/driver_gap_$TAG.json" ;;
     probe) run cp_pingpong_$TAG 120 tools/probes/cp_pingpong 2000 ;;
+    handoff) run kernel_handoff_$TAG 120 tools/probes/kernel_handoff 2000 ;;
     jsbsim)  # is a JSBSim binding present on the box? (probe only; never installed)
       python -c "import jsbsim, sys; print('jsbsim', jsbsim.__version__)" > "$OUT/jsbsim_probe_$TAG.log" 2>&1
       echo "[session] jsbsim probe rc=$?"; tail -2 "$OUT/jsbsim_probe_$TAG.log" ;;
