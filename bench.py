@@ -697,7 +697,7 @@ def main():
             "traffic": traffic,
             "valu": None if cfg5 else load_valu(n, args.stack, kernel_name),
             # cfg5: auto-resets happen inside the step kernel from the reset cache, which
-            # f16_ic_fill_kernel refills every F16ENV_ICC_PERIOD (32) steps
+            # f16_ic_fill_kernel refills every F16ENV_ICC_PERIOD (64) steps
             "kernel": kernel_name + (" + f16_ic_fill_kernel (reset cache refill)" if cfg5 else ""),
             "waves_per_simd": waves_per_simd,
             "kernel_ms": round(roof_ms, 5),

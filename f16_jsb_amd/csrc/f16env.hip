@@ -1864,7 +1864,7 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   h->done_buf = nullptr;
   h->icc.c = nullptr; h->icc.n = cfg->n_envs;
   h->icc_steps = 0;
-  h->icc_period = 32;
+  h->icc_period = 64;  // same-box sweep, 2 048 cfg5 steps: 27.5 / 27.0 / 27.0 / 26.8 / 27.7 us at 32..512
   if (getenv("F16ENV_ICC_PERIOD")) h->icc_period = atoi(getenv("F16ENV_ICC_PERIOD"));
   if (hipMalloc(&h->tmem, (size_t)TMPL_COLS * 16) != hipSuccess ||
       hipMalloc((void**)&h->ic_dev, sizeof(double) * 3 * F16_IC_N) != hipSuccess ||

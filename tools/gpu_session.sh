@@ -64,6 +64,10 @@ for s in $STEPS; do
       python -c "import jsbsim, sys; print('jsbsim', jsbsim.__version__)" > "$OUT/jsbsim_probe_$TAG.log" 2>&1
       echo "[session] jsbsim probe rc=$?"; tail -2 "$OUT/jsbsim_probe_$TAG.log" ;;
     stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
+    iccsweep)  # cfg5 reset-cache refill period, same box
+      for P in ${ICC_PERIODS:-8 16 32 64 128}; do
+        F16ENV_ICC_PERIOD=$P run bench_cfg5_icc${P}_$TAG 300 python bench.py --workload cfg5 --steps ${ICC_STEPS:-300} --warmup 20 --no-cpu-baseline
+      done ;;
     bench5) run bench_cfg5_$TAG 600 python bench.py --workload cfg5 --steps 300 --warmup 20 --cpu-seconds 5 ;;
     variants) run variant_sweep 900 python tools/variant_sweep.py run --json "$OUT/variants_$TAG.json" ;;
     div) run cfg5_divergence_$TAG 900 python tests/cfg5_divergence.py --n 4096 --json "$OUT/cfg5_divergence_$TAG.json" ;;
