@@ -2442,11 +2442,11 @@ const char* f16env_step_kernel_name(f16env_t h) {
   if (h->wb.hist[0]) {
     snprintf(buf, sizeof buf, "f16_step_win%s_kernel<%d, %d>", h->win_nt ? "_nt" : "", h->mode & 3, h->win_occ);
   } else if (h->gt) {
-    snprintf(buf, sizeof buf, "f16_step_gt_kernel<%d>", h->mode & 3);
+    snprintf(buf, sizeof buf, "f16_step_gt_kernel<%d, false>", h->mode & 3);  // as rocprofv3 demangles it
   } else if ((h->mode & 3) == 0 && h->occ == 1) {
     snprintf(buf, sizeof buf, "f16_step_kernel");
   } else {
-    snprintf(buf, sizeof buf, "f16_step_var_kernel<%d, %d>", h->mode & 3, h->occ);
+    snprintf(buf, sizeof buf, "f16_step_var_kernel<%d, %d, false>", h->mode & 3, h->occ);
   }
   return buf;
 }

@@ -161,7 +161,7 @@ def test_cfg5_production_instance_131072(torch_mod, layout, done_list):
     n = 131072
     ref = OracleEnvs(n, stack_k=4, seed=41, cfg5=True)
     g = F16Envs(n, stack_k=4, seed=41, cfg5=True, obs_layout=layout)
-    want = "f16_step_win_nt_kernel<3, 2>" if layout == "window" else "f16_step_var_kernel<3, 2>"
+    want = "f16_step_win_nt_kernel<3, 2>" if layout == "window" else "f16_step_var_kernel<3, 2, false>"
     assert g.step_kernel_name == want, g.step_kernel_name
     assert g.waves_per_simd == 2
     o = ref.reset()
@@ -193,7 +193,7 @@ def test_reference_stack_k10_global_table_instance(torch_mod):
     from f16_jsb_amd.env import F16Envs
     n = 4096
     ref, g = OracleEnvs(n, stack_k=10, seed=51), F16Envs(n, stack_k=10, seed=51)
-    assert g.step_kernel_name == "f16_step_gt_kernel<0>", g.step_kernel_name
+    assert g.step_kernel_name == "f16_step_gt_kernel<0, false>", g.step_kernel_name
     o = ref.reset()
     o_g = g.reset().cpu().numpy()
     np.testing.assert_array_equal(o_g[:, :, 12:], o[:, :, 12:])

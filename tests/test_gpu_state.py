@@ -76,7 +76,7 @@ def test_wind_by_set_state_switches_kernels(torch_mod):
     ref.set_state(s)
     g.set_state(s)
     g.set_obs(o)
-    assert g.step_kernel_name == "f16_step_var_kernel<2, 1>"
+    assert g.step_kernel_name == "f16_step_var_kernel<2, 1, false>"
     _run_parity(torch_mod, ref, g, 30, 6, TOL_RAND30)
 
 
@@ -90,7 +90,7 @@ def test_wind_by_reset_ic_switches_kernels(torch_mod):
     o_r = ref.reset(goals=goals, ic=ic)
     o_g = g.reset(goals=goals, ic=ic).cpu().numpy()
     _assert_frames(o_g[:, -1], o_r[:, -1], TOL_STEP, "IC frame")
-    assert g.step_kernel_name == "f16_step_var_kernel<2, 1>"
+    assert g.step_kernel_name == "f16_step_var_kernel<2, 1, false>"
     _run_parity(torch_mod, ref, g, 30, 9, TOL_RAND30)
 
 
@@ -99,7 +99,7 @@ def test_config_wind_selects_wind_kernels(torch_mod):
     ic = default_ic()
     ic[F16_IC_WIND_N_FPS] = 12.0
     g = F16Envs(64, stack_k=4, seed=1, ic=ic)
-    assert g.step_kernel_name == "f16_step_var_kernel<2, 1>"
+    assert g.step_kernel_name == "f16_step_var_kernel<2, 1, false>"
     g.reset()
     s = g.get_state().cpu().numpy()
     assert np.all(s[:, F16C_WIND] == 12.0)
