@@ -238,13 +238,14 @@ __device__ __forceinline__ float without_sign_flag(float v) { return __uint_as_f
 // derive's, so the recomputed latch equals the one the last frame of the previous step held)
 __device__ __forceinline__ void pqr_aero(const float* q, const float* wI, float* pqr) {
   const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-  const float T2 = 2.0f * (q1 * q3 - q0 * q2);
-  const float T5 = 2.0f * (q2 * q3 + q0 * q1);
-  const float T8 = q0 * q0 - q1 * q1 - q2 * q2 + q3 * q3;
+  // explicit FMAs: the same rounding in every build that inlines it (see derive)
+  const float T2 = 2.0f * __builtin_fmaf(q1, q3, -(q0 * q2));
+  const float T5 = 2.0f * __builtin_fmaf(q2, q3, q0 * q1);
+  const float T8 = __builtin_fmaf(q3, q3, __builtin_fmaf(-q2, q2, __builtin_fmaf(-q1, q1, q0 * q0)));
   const float we = (float)0.00007292115;
-  pqr[0] = wI[0] - T2 * we;
-  pqr[1] = wI[1] - T5 * we;
-  pqr[2] = wI[2] - T8 * we;
+  pqr[0] = __builtin_fmaf(-T2, we, wI[0]);
+  pqr[1] = __builtin_fmaf(-T5, we, wI[1]);
+  pqr[2] = __builtin_fmaf(-T8, we, wI[2]);
 }
 // ground speed (FGAuxiliary Vground): horizontal part of the velocity wrt the rotating Earth,
 // |v|^2 - (v . r_hat)^2 with r_hat the geocentric up (the local frame's down axis is -r_hat).
@@ -426,14 +427,14 @@ __device__ __forceinline__ float fatan2(float y, float x) {
   const float a = (mx > 0.0f) ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
   const float s = a * a;
   float p = 2.4566815505e-03f;
-  p = p * s - 1.4401176748e-02f;
-  p = p * s + 3.9780909971e-02f;
-  p = p * s - 7.2348286170e-02f;
-  p = p * s + 1.0498931099e-01f;
-  p = p * s - 1.4161224781e-01f;
-  p = p * s + 1.9985906079e-01f;
-  p = p * s - 3.3332596980e-01f;
-  p = p * s + 9.9999988637e-01f;
+  p = __builtin_fmaf(p, s, -1.4401176748e-02f);
+  p = __builtin_fmaf(p, s, 3.9780909971e-02f);
+  p = __builtin_fmaf(p, s, -7.2348286170e-02f);
+  p = __builtin_fmaf(p, s, 1.0498931099e-01f);
+  p = __builtin_fmaf(p, s, -1.4161224781e-01f);
+  p = __builtin_fmaf(p, s, 1.9985906079e-01f);
+  p = __builtin_fmaf(p, s, -3.3332596980e-01f);
+  p = __builtin_fmaf(p, s, 9.9999988637e-01f);
   float r = a * p;
   r = (ay > ax) ? 1.57079632679489662f - r : r;
   r = (x < 0.0f) ? 3.14159265358979324f - r : r;
@@ -606,16 +607,17 @@ struct Derived {
 
 __device__ __forceinline__ void quat_T(const float* q, float* T) {
   const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-  const float q0q0 = q0 * q0, q1q1 = q1 * q1, q2q2 = q2 * q2, q3q3 = q3 * q3;
-  T[0] = q0q0 + q1q1 - q2q2 - q3q3;
-  T[1] = 2.0f * (q1 * q2 + q0 * q3);
-  T[2] = 2.0f * (q1 * q3 - q0 * q2);
-  T[3] = 2.0f * (q1 * q2 - q0 * q3);
-  T[4] = q0q0 - q1q1 + q2q2 - q3q3;
-  T[5] = 2.0f * (q2 * q3 + q0 * q1);
-  T[6] = 2.0f * (q1 * q3 + q0 * q2);
-  T[7] = 2.0f * (q2 * q3 - q0 * q1);
-  T[8] = q0q0 - q1q1 - q2q2 + q3q3;
+  // explicit FMAs: the same rounding in every build that inlines it (see derive)
+  const float q0q0 = q0 * q0;
+  T[0] = __builtin_fmaf(-q3, q3, __builtin_fmaf(-q2, q2, __builtin_fmaf(q1, q1, q0q0)));
+  T[1] = 2.0f * __builtin_fmaf(q1, q2, q0 * q3);
+  T[2] = 2.0f * __builtin_fmaf(q1, q3, -(q0 * q2));
+  T[3] = 2.0f * __builtin_fmaf(q1, q2, -(q0 * q3));
+  T[4] = __builtin_fmaf(-q3, q3, __builtin_fmaf(q2, q2, __builtin_fmaf(-q1, q1, q0q0)));
+  T[5] = 2.0f * __builtin_fmaf(q2, q3, q0 * q1);
+  T[6] = 2.0f * __builtin_fmaf(q1, q3, q0 * q2);
+  T[7] = 2.0f * __builtin_fmaf(q2, q3, -(q0 * q1));
+  T[8] = __builtin_fmaf(q3, q3, __builtin_fmaf(-q2, q2, __builtin_fmaf(-q1, q1, q0q0)));
 }
 __device__ __forceinline__ void mmul(const float* A, const float* B, float* C) {
 #pragma unroll
@@ -741,8 +743,8 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
   // position: the same rotations as ECEF -> local composed with Ti2b * Tec2i, without
   // forming Tec2b (FGPropagate's Tec2b and Tec2l products). fp32 direction cosines.
   const float xi = (float)L.rI[0], yi = (float)L.rI[1], zf = (float)zE;
-  const float rxyf = fsqrt(xi * xi + yi * yi);
-  const float rf = fsqrt(rxyf * rxyf + zf * zf);
+  const float rxyf = fsqrt(__builtin_fmaf(xi, xi, yi * yi));
+  const float rf = fsqrt(__builtin_fmaf(rxyf, rxyf, zf * zf));
   const float inv_r = rcpf(rf);
   const float slat = zf * inv_r, clat = rxyf * inv_r;
   float slon = 0.0f, clon = 1.0f;  // of the ECI position (Earth longitude + Earth angle)
@@ -760,9 +762,12 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float a = d.Ti2b[3 * i], b = d.Ti2b[3 * i + 1], e = d.Ti2b[3 * i + 2];
-    d.Tl2b[3 * i] = a * L0 + b * L1 + e * L2;
-    d.Tl2b[3 * i + 1] = a * L3 + b * L4;
-    d.Tl2b[3 * i + 2] = a * L6 + b * L7 + e * L8;
+    // explicit FMAs (as in euler / fatan2 / make_frame_from): the observation's Euler angles
+    // come out of these, and compiler-chosen contraction paired them differently in the one-
+    // and two-waves-per-SIMD windowed builds (last-bit phi / theta / psi differences)
+    d.Tl2b[3 * i] = __builtin_fmaf(e, L2, __builtin_fmaf(b, L1, a * L0));
+    d.Tl2b[3 * i + 1] = __builtin_fmaf(b, L4, a * L3);
+    d.Tl2b[3 * i + 2] = __builtin_fmaf(e, L8, __builtin_fmaf(b, L7, a * L6));
   }
   // vUVW = Ti2b * (vI - w x rI)
   const float vr[3] = {(float)(L.vI[0] + OMEGA_E * L.rI[1]), (float)(L.vI[1] - OMEGA_E * L.rI[0]),
@@ -797,7 +802,7 @@ __device__ __forceinline__ void euler(const float* T, float& phi, float& tht, fl
   } else {
     // theta = asin(-T13) as atan2(-T13, cos theta) with cos theta = |(T23, T33)| (Tl2b is a
     // rotation); the polynomial atan2 (|err| < 1e-7 rad) instead of OCML's asinf / atan2f
-    tht = fatan2(-T[2], fsqrt(T[5] * T[5] + T[8] * T[8]));
+    tht = fatan2(-T[2], fsqrt(__builtin_fmaf(T[5], T[5], T[8] * T[8])));
     phi = fatan2(T[5], T[8]);
     float p = fatan2(T[1], T[0]);
     if (p < 0.0f) p += 2.0f * PI_F;

@@ -256,10 +256,14 @@ __device__ __forceinline__ float norm_angle(float a) {
 // two builds then round the observation differently: kept out, the one- and two-waves-per-
 // SIMD builds stay bit-identical.)
 __device__ void make_frame_from(const Lane& L, double ce, double se, const Derived& d, float* f) {
-  const double xE = ce * L.rI[0] + se * L.rI[1];
-  const double yE = -se * L.rI[0] + ce * L.rI[1];
+  // explicit FMAs: with contraction left to the compiler, the one- and two-waves-per-SIMD
+  // windowed builds paired these products differently, and yE (a difference of two ~2e7 ft
+  // terms near the start meridian) and so the observed longitude differed in the last bits
+  // (tests/test_gpu_production.py two-million-env case)
+  const double xE = __builtin_fma(ce, L.rI[0], se * L.rI[1]);
+  const double yE = __builtin_fma(ce, L.rI[1], -se * L.rI[0]);
   const float xf = (float)xE, yf = (float)yE, zf = (float)L.rI[2];
-  const float rxyE = fsqrt(xf * xf + yf * yf);
+  const float rxyE = fsqrt(__builtin_fmaf(xf, xf, yf * yf));
   const float lat = atan2f(zf, rxyE);
   const float lon = (rxyE == 0.0f) ? 0.0f : atan2f(yf, xf);
   float phi, tht, psi;

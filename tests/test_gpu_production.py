@@ -299,3 +299,39 @@ def test_shard_invariance_one_vs_two_handles(torch_mod, cfg5):
     assert torch.equal(torch.cat([p.get_state() for p in parts]), sb)
     for x in [big] + parts:
         x.close()
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "window"])
+@pytest.mark.parametrize("cfg5", [False, True], ids=["reference_task", "cfg5"])
+def test_two_million_env_grid_tail_matches_its_shard(torch_mod, layout, cfg5):
+    """Maximum-size indexing: 2^21 + 77 envs in ONE handle (64-bit column offsets past 2^31
+    bytes, grids of several rounds of waves, a ragged last wave). Its last 333 lanes must step
+    bit-identically to a 333-env handle holding the same global env ids (env_id_base =
+    N - 333): actions, observations, rewards, flags and final state, over 90 steps with
+    max_steps 40 (every lane truncates and auto-resets twice) and, in cfg5 mode, random-IC
+    crashes and in-step cached resets (window layout). The two handles run different kernel
+    instances (grid size picks them), which round identically."""
+    torch = torch_mod
+    from f16_jsb_amd.env import F16Envs
+    n, tail = (1 << 21) + 77, 333
+    kw = dict(stack_k=4, seed=93, cfg5=cfg5, max_steps=40, obs_layout=layout,
+              **({"history": 16} if layout == "window" else {}))
+    big = F16Envs(n, env_id_base=0, **kw)
+    small = F16Envs(tail, env_id_base=n - tail, **kw)
+    ob, os_ = big.reset(), small.reset()
+    assert torch.equal(ob[n - tail:], os_)
+    resets = 0
+    for t in range(90):
+        a = big.sample_actions(5, t)
+        a_s = small.sample_actions(5, t)
+        assert torch.equal(a[n - tail:], a_s)
+        o_b, o_s = big.step(a), small.step(a_s)
+        assert torch.equal(o_b.obs[n - tail:], o_s.obs), "obs @%d" % t
+        assert torch.equal(o_b.rew[n - tail:], o_s.rew), "rew @%d" % t
+        assert torch.equal(o_b.terminated[n - tail:], o_s.terminated)
+        assert torch.equal(o_b.truncated[n - tail:], o_s.truncated)
+        resets += int((o_s.terminated | o_s.truncated).bool().sum())
+    assert resets >= 2 * tail
+    assert torch.equal(big.get_state()[n - tail:], small.get_state())
+    big.close()
+    small.close()
