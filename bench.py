@@ -608,7 +608,7 @@ def main():
     # dispatch packet (hipExtLaunchKernel, f16env_profile_*) on the launch stream, over a
     # second pass of the same steps -- the kernel's execution, as rocprofv3's kernel trace
     # measures it, without the dependent-launch boundary the timed region above includes
-    nk = min(args.steps, 500)
+    nk = max(200, min(args.steps, 500))  # >= 200 launches: a 20-step run's mean is one outlier away from noise
 
     def second_pass():
         for t in range(nk):

@@ -39,7 +39,13 @@ def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = Fa
     # kernarg preload (gfx950): the first 8 argument dwords arrive in SGPRs at wave start; the
     # windowed step kernels take their prologue's addresses there (StepPre): 65 536 envs kernel
     # 16.51 -> 16.19 us (two same-box A/Bs, profiles/r02_variants_preload.txt)
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
+    # -ffp-contract=on: a*b+c is fused per source expression by the front end (llvm.fmuladd),
+    # not by the backend's per-kernel pattern matching, so every template instance rounds the
+    # same expression the same way: the contiguous and windowed layouts and the one- / two-
+    # waves-per-SIMD builds are bit-identical (with =fast, HIP's default, a cfg5 lane in 65 536
+    # diverged by step 4 between layouts; step kernel time unchanged, tools/diag/con_ab.sh)
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on", "-shared", "-fPIC",
+           "-fno-slp-vectorize",
            "-mllvm", "-amdgpu-kernarg-preload-count=8",
            "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
            SRC, "-o", out + ".tmp", *extra]

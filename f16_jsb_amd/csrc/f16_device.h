@@ -624,22 +624,28 @@ __device__ __forceinline__ void mmul(const float* A, const float* B, float* C) {
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+      C[3 * i + j] = __builtin_fmaf(A[3 * i + 2], B[6 + j], __builtin_fmaf(A[3 * i + 1], B[3 + j], A[3 * i] * B[j]));
+}
+// Explicit FMAs in the small products: left to the compiler, contraction is chosen per
+// kernel instance, and the contiguous and windowed cfg5 builds then rounded the wind-axis
+// velocity differently (tools/diag/layout_identity.py)
+__device__ __forceinline__ float dot3f(float a0, float b0, float a1, float b1, float a2, float b2) {
+  return __builtin_fmaf(a2, b2, __builtin_fmaf(a1, b1, a0 * b0));
 }
 __device__ __forceinline__ void mvec(const float* M, const float* v, float* o) {
-  o[0] = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
-  o[1] = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
-  o[2] = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+  o[0] = dot3f(M[0], v[0], M[1], v[1], M[2], v[2]);
+  o[1] = dot3f(M[3], v[0], M[4], v[1], M[5], v[2]);
+  o[2] = dot3f(M[6], v[0], M[7], v[1], M[8], v[2]);
 }
 __device__ __forceinline__ void mtvec(const float* M, const float* v, float* o) {
-  o[0] = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
-  o[1] = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
-  o[2] = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+  o[0] = dot3f(M[0], v[0], M[3], v[1], M[6], v[2]);
+  o[1] = dot3f(M[1], v[0], M[4], v[1], M[7], v[2]);
+  o[2] = dot3f(M[2], v[0], M[5], v[1], M[8], v[2]);
 }
 __device__ __forceinline__ void crossf(const float* a, const float* b, float* o) {
-  const float x = a[1] * b[2] - a[2] * b[1];
-  const float y = a[2] * b[0] - a[0] * b[2];
-  const float z = a[0] * b[1] - a[1] * b[0];
+  const float x = __builtin_fmaf(a[1], b[2], -(a[2] * b[1]));
+  const float y = __builtin_fmaf(a[2], b[0], -(a[0] * b[2]));
+  const float z = __builtin_fmaf(a[0], b[1], -(a[1] * b[0]));
   o[0] = x; o[1] = y; o[2] = z;
 }
 
@@ -736,7 +742,7 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
   const double zE = L.rI[2];
   {
     const float dx = (float)(xE - A.r0[0]), dy = (float)(yE - A.r0[1]), dz = (float)(zE - A.r0[2]);
-    d.h_ft = A.h0 + (double)(A.n[0] * dx + A.n[1] * dy + A.n[2] * dz);
+    d.h_ft = A.h0 + (double)__builtin_fmaf(A.n[2], dz, __builtin_fmaf(A.n[1], dy, A.n[0] * dx));
   }
   // The local NED frame (FGLocation's, geocentric) and J2 gravity (FGInertial::GetGravityJ2)
   // are symmetric about the Earth's axis, so they are evaluated in ECI axes from the ECI

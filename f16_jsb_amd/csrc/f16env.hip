@@ -699,7 +699,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       rng_normals(a.E.seed, (uint64_t)(a.E.id_base + k), (uint32_t)(L.ep_count - 1), (uint32_t)L.step, xi);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        L.gust[j] = a.E.gust_a * L.gust[j] + a.E.gust_b * xi[j];
+        L.gust[j] = __builtin_fmaf(a.E.gust_a, L.gust[j], a.E.gust_b * xi[j]);  // explicit: every build alike
         L.wind[j] = L.wst[j] + L.gust[j];
       }
     }

@@ -74,8 +74,18 @@ def test_fp64_self_differences_are_derive_reference_point():
         if not m or m.group(4) != m.group(6) or m.group(3) == m.group(5):
             continue
         seen += 1
-        cvt = re.compile(r"\bv_cvt_f32_f64(_e32|_e64)?\s+v\d+, " + re.escape(m.group(2)) + r"(\s|$)")
-        if not any(cvt.search(nxt) for nxt in lines[i + 1:i + 40]):
+        # the next instruction that reads the difference must be its narrowing, and it must
+        # come before anything overwrites it (scheduling can put many instructions between)
+        reg = re.escape(m.group(2))
+        cvt = re.compile(r"\bv_cvt_f32_f64(_e32|_e64)?\s+v\d+, " + reg + r"(\s|$)")
+        ok = False
+        for nxt in lines[i + 1:i + 400]:
+            if cvt.search(nxt):
+                ok = True
+                break
+            if re.search(reg, nxt):  # any other read or a redefinition first
+                break
+        if not ok:
             bad.append(line.strip())
     assert not bad, "fp64 x - x not narrowed to fp32 (not derive's reference-point difference): %s" % bad[:4]
     assert seen > 0  # the pattern matches the disassembler's syntax (derive's are in there)
