@@ -1107,9 +1107,8 @@ static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {
 // frames in an LDS ring across the whole rollout, and per step writes only the rollout slot
 // (newest frame of the observation acted on, action, reward, next episode start). State and
 // the final observation stack are stored once, at the end. Same arithmetic, RNG streams and
-// auto-reset as T launches of the fused step (f16env_step_rollout): identical actions and
-// episode starts, frames and rewards equal up to fp32 rounding (compiled in another kernel,
-// a few products contract differently).
+// auto-reset as T launches of the fused step (f16env_step_rollout): bit-identical results
+// (build.py -ffp-contract=on: contraction is fixed per source expression, not per kernel).
 // ------------------------------------------------------------------------------------------
 struct RollArgs {
   SoA s, tmpl;
