@@ -688,8 +688,8 @@ def main():
             # the path has no dense contraction, so the roof the fraction is quoted against is HBM
             # (BASELINE.json); the kernel itself is latency-bound: one wave per SIMD at 65 536 envs,
             # neither HBM (frac) nor VALU issue (valu.valu_busy_frac) saturated
-            "bound": "latency",
-            "roof": "hbm",
+            "bound": "hbm",
+            "limiter": "latency (one wave per SIMD: neither HBM nor VALU issue saturated)",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
