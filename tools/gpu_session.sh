@@ -57,6 +57,9 @@ for s in $STEPS; do
     dist2)  # the bench's N > 1 code path with 2 ranks sharing this box's GPU (gloo: rehearsal only)
       run bench_dist2_$TAG 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
+    soak)  # long runs at the bench's sizes: product build, then the bounds-checked debug build
+      run soak_$TAG 600 python tools/soak.py
+      F16ENV_LIB=f16_jsb_amd/libf16env_debug.so run soak_debug_$TAG 900 python tools/soak.py --steps3 5000 --steps5 3000 ;;
     gap) run driver_gap_$TAG 300 python tools/driver_gap.py --json "$OUT/driver_gap_$TAG.json" ;;
     probe) run cp_pingpong_$TAG 120 tools/probes/cp_pingpong 2000 ;;
     handoff) run kernel_handoff_$TAG 120 tools/probes/kernel_handoff 2000 ;;
