@@ -2,7 +2,9 @@
 # One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel-trace summary.
 # Each step has its own time limit; a step that faults / aborts / times out ends the session
 # (pytest's "tests failed" exit 1 does not). Output lands in gpurun_out/.
-#   usage: tools/gpu_session.sh [tag] [steps...]   steps: tests smoke bench prof pmc report
+#   usage: tools/gpu_session.sh [tag] [steps...]
+#   steps: tests prodtests smoke bench driver profdrv bench5 dist2 soak gap probe handoff jsbsim
+#          stamps iccsweep variants div sweep report prof sq pmc   (default: tests smoke bench prof)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
