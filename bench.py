@@ -492,10 +492,10 @@ def layout_leg(dev, args, layout, steps=300):
     return out
 
 
-def load_traffic(envs, stack, state_bytes, layout):
+def load_traffic(envs, stack, state_bytes, layout, name="pmc_traffic.json"):
     """Per-launch HBM bytes of the step kernel from the committed PMC summary, if it was
-    measured on this workload, state size and observation layout."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    measured on this workload, state size and observation layout (cfg5: pmc_traffic_cfg5.json)."""
+    p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
@@ -656,7 +656,8 @@ def main():
     # (cfg5: the step is two kernels -- step + deferred reset -- so the region time is used)
     roof_ms = gpu_ms_per_step if cfg5 else kern_ms
     achieved = bytes_per_launch / (roof_ms * 1e-3) / 1e9
-    traffic = None if cfg5 else load_traffic(n, args.stack, envs.state_bytes_per_env, args.obs_layout)
+    traffic = load_traffic(n, args.stack, envs.state_bytes_per_env, args.obs_layout,
+                           "pmc_traffic_cfg5.json" if cfg5 else "pmc_traffic.json")
     out = {
         "metric": METRIC,
         "value": round(value, 1),

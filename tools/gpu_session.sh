@@ -88,6 +88,11 @@ for s in $STEPS; do
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_sq3 600 rocprofv3 --pmc SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 -d "$OUT/pmc_sq3_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0 ;;
+    pmc5)  # HBM traffic of the cfg5 step kernel (summary: tools/pmc_traffic.py ... --envs 131072 --extra-bytes 24)
+      run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc5_fetch_$TAG" -o run --output-format csv -- \
+        python bench.py --workload cfg5 --steps 50 --warmup 5 --no-cpu-baseline
+      run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc5_write_$TAG" -o run --output-format csv -- \
+        python bench.py --workload cfg5 --steps 50 --warmup 5 --no-cpu-baseline ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0

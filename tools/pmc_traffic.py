@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--kernel", default="f16_step_win_kernel")
     ap.add_argument("--layout", default="window", choices=("window", "contiguous"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--extra-bytes", type=int, default=0,
+                    help="per env step on top of the layout's bytes (cfg5: 24, the gust state's read + write, as bench.py)")
     a = ap.parse_args()
     from f16_jsb_amd._lib import lib
     from f16_jsb_amd.abi import algorithmic_bytes_per_env_step
@@ -45,10 +47,11 @@ def main():
     rd = 2.0 * fetch_kib * 1024.0
     wr = write_kib * 1024.0
     state_bytes = int(lib().f16env_state_bytes_per_env())
-    alg = algorithmic_bytes_per_env_step(a.stack, state_bytes) * a.envs
-    lay = algorithmic_bytes_per_env_step(a.stack, state_bytes, a.layout) * a.envs  # this layout's own
+    alg = (algorithmic_bytes_per_env_step(a.stack, state_bytes) + a.extra_bytes) * a.envs
+    lay = (algorithmic_bytes_per_env_step(a.stack, state_bytes, a.layout) + a.extra_bytes) * a.envs  # this layout's
     d = {
         "kernel": a.kernel, "layout": a.layout, "envs": a.envs, "stack_k": a.stack, "state_bytes": state_bytes,
+        "extra_bytes_per_env_step": a.extra_bytes,
         "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib, "launches": [nf, nw],
         "hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
         "hbm_bytes_per_launch": int(rd + wr),
