@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--rollout-envs", type=int, default=32768, help="cfg4 rollout envs per GPU (0 = skip)")
     ap.add_argument("--rollout-steps", type=int, default=2048, help="cfg4 PPO n_steps")
     ap.add_argument("--gather-chunk", type=int, default=256, help="steps per RCCL gather chunk")
+    ap.add_argument("--policy-steps", type=int, default=256,
+                    help="rollout leg: steps of the policy-in-the-loop rollout (0 = skip)")
     ap.add_argument("--burn-in", type=int, default=None,
                     help="untimed steps after the phase spread (default: max_steps = 1200) so the timed window "
                          "sees the steady-state episode mix (crashes, goals, truncations, auto-resets)")
@@ -188,20 +190,73 @@ def spread_phases(envs, args, dev):
     return {"phase_spread": "step counters uniform over [0, %d)" % max_steps, "burn_in_steps": burn}
 
 
+class MlpActorCritic:
+    """The policy of the rollout leg's policy-in-the-loop rate: SB3's default PPO MlpPolicy shape
+    (stable_baselines3 ActorCriticPolicy: flattened observation -> separate pi / vf MLPs
+    [64, 64] with tanh, a 4-wide action mean with a state-independent log std, a value head;
+    actions sampled from the diagonal Gaussian, their log-probability summed over the action
+    dims), random-init weights. __call__(obs) -> (actions, values, log_probs) as
+    on_policy_algorithm.py:202's policy(obs_tensor); value(obs) the vf branch alone."""
+
+    def __init__(self, obs_dim, dev, seed=0):
+        import torch
+        g = torch.Generator(device="cpu").manual_seed(seed)
+
+        def lin(i, o, gain):
+            w = torch.randn(o, i, generator=g) * (gain / i ** 0.5)
+            return w.to(dev), torch.zeros(o, device=dev)
+
+        self.pi = [lin(obs_dim, 64, 2 ** 0.5), lin(64, 64, 2 ** 0.5)]
+        self.vf = [lin(obs_dim, 64, 2 ** 0.5), lin(64, 64, 2 ** 0.5)]
+        self.act_w = lin(64, 4, 0.01)
+        self.val_w = lin(64, 1, 1.0)
+        self.log_std = torch.zeros(4, device=dev)
+
+    @staticmethod
+    def _mlp(x, layers):
+        import torch
+        for w, b in layers:
+            x = torch.tanh(torch.nn.functional.linear(x, w, b))
+        return x
+
+    def value(self, obs):
+        import torch
+        x = obs.reshape(obs.shape[0], -1)
+        return torch.nn.functional.linear(self._mlp(x, self.vf), *self.val_w).reshape(-1)
+
+    def __call__(self, obs):
+        import math
+        import torch
+        x = obs.reshape(obs.shape[0], -1)
+        mean = torch.nn.functional.linear(self._mlp(x, self.pi), *self.act_w)
+        std = self.log_std.exp()
+        eps = torch.randn_like(mean)
+        act = mean + std * eps
+        logp = (-0.5 * eps * eps - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+        return act, self.value(obs), logp
+
+
 def rollout_bench(args, dev, rank, world):
     """BASELINE cfg4 beside the headline: a PPO-shaped rollout (n_steps x envs per GPU) into
     the device rollout buffer, HIP GAE, then the RCCL gather of every shard to rank 0.
-    Rollout, GAE and gather are timed separately (max over ranks); not part of `value`."""
+    Rollout, GAE and gather are timed separately (max over ranks); not part of `value`.
+    The envs step in the windowed layout (the headline's); the rollout is timed three ways:
+    the random policy as ONE persistent launch (f16env_window_rollout_random), the random policy
+    as one fused rollout-step launch per step (f16env_window_step_rollout, actions drawn
+    in-kernel; beside it the plain windowed step at the same env count, and the contiguous
+    layout's fused steps), and a policy network in the loop (MlpActorCritic: SB3's default
+    PPO policy shape, its actions clipped in-kernel, the timeout bootstrap on device)."""
     import torch
     import torch.distributed as dist
     from f16_jsb_amd.env import F16Envs
     from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout, gather_to_rank0
 
     n, T = args.rollout_envs, args.rollout_steps
-    envs = F16Envs(n, stack_k=args.stack, device=dev, seed=args.seed + 7, env_id_base=rank * n)
+    envs = F16Envs(n, stack_k=args.stack, device=dev, seed=args.seed + 7, env_id_base=rank * n, obs_layout="window")
     envs.reset()
     buf = DeviceRolloutBuffer(T, n, args.stack, dev)
     collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), args.seed + 3000)  # warm
+    collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), args.seed + 3000, persistent=False)
     sync = torch.cuda.synchronize
 
     def barrier():
@@ -209,12 +264,20 @@ def rollout_bench(args, dev, rank, world):
             dist.barrier()
         sync()
 
-    # the same rollout as one fused launch per step (f16env_step_rollout), for comparison
+    # the same rollout as one fused launch per step (f16env_window_step_rollout), for comparison
     barrier()
     tf0 = time.perf_counter()
     collect_rollout(envs, buf, args.seed + 5000, persistent=False)
     sync()
     fused_s = time.perf_counter() - tf0
+    # the plain windowed step at the same env count (what the fused rollout step adds to)
+    acts = [envs.sample_actions(args.seed + 5500, t) for t in range(8)]
+    sync()
+    tp0 = time.perf_counter()
+    for t in range(512):
+        envs.step(acts[t % 8])
+    sync()
+    plain_ms = (time.perf_counter() - tp0) / 512 * 1e3
     barrier()
     t0 = time.perf_counter()
     last_v, last_d = collect_rollout(envs, buf, args.seed + 4000)  # one persistent launch
@@ -223,6 +286,59 @@ def rollout_bench(args, dev, rank, world):
     buf.compute_returns_and_advantage(last_v, last_d)
     sync()
     t2 = time.perf_counter()
+    # GAE kernel alone: HIP events on the launch stream, 5 launches
+    stream = torch.cuda.current_stream(dev)
+    ge0, ge1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ge0.record(stream)
+    for _ in range(5):
+        buf.compute_returns_and_advantage(last_v, last_d)
+    ge1.record(stream)
+    sync()
+    gae_kernel_ms = ge0.elapsed_time(ge1) / 5
+    gae_bytes = T * n * 20 + n * 5  # rewards, values, starts read; advantages, returns written; last values, dones
+    # the contiguous layout's fused rollout steps (round 3's per-step path)
+    cont = {}
+    if world == 1:
+        ec = F16Envs(n, stack_k=args.stack, device=dev, seed=args.seed + 7, obs_layout="contiguous")
+        ec.reset()
+        collect_rollout(ec, DeviceRolloutBuffer(8, n, args.stack, dev), args.seed + 3000, persistent=False)
+        sync()
+        tc0 = time.perf_counter()
+        collect_rollout(ec, buf, args.seed + 5000, persistent=False)
+        sync()
+        cont = {"rollout_fused_contiguous_s": round(time.perf_counter() - tc0, 4)}
+        ec.close()
+    # policy in the loop (on_policy_algorithm.py:194-262 with a policy network)
+    pol = {}
+    if args.policy_steps > 0:
+        net = MlpActorCritic(args.stack * 15, dev, seed=args.seed)
+        pbuf = DeviceRolloutBuffer(args.policy_steps, n, args.stack, dev)
+        with torch.no_grad():
+            collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), policy_fn=net, value_fn=net.value)
+            barrier()
+            tq0 = time.perf_counter()
+            lv, ld = collect_rollout(envs, pbuf, policy_fn=net, value_fn=net.value)
+            pbuf.compute_returns_and_advantage(lv, ld)
+            sync()
+            pol_s = time.perf_counter() - tq0
+            # the policy's share: its forward + the terminal-value forward alone, same batch
+            o = envs.obs
+            for _ in range(3):
+                net(o), net.value(o)
+            sync()
+            tq1 = time.perf_counter()
+            for _ in range(50):
+                net(o), net.value(o)
+            sync()
+            policy_ms = (time.perf_counter() - tq1) / 50 * 1e3
+        pol = {"policy_in_the_loop": {
+            "policy": "MlpActorCritic (SB3 default PPO MlpPolicy shape: pi/vf [64, 64] tanh, Gaussian, random init), "
+                      "torch eager on the window view, actions clipped in-kernel, timeout bootstrap on device",
+            "steps": args.policy_steps, "rollout_plus_gae_s": round(pol_s, 4),
+            "env_steps_per_s": round(n * world * args.policy_steps / pol_s, 1),
+            "ms_per_step": round(pol_s / args.policy_steps * 1e3, 5),
+            "policy_forward_ms_per_step": round(policy_ms, 5)}}
+        del pbuf
     gathered = 0
     t_gather = 0.0
     if world > 1:
@@ -236,22 +352,33 @@ def rollout_bench(args, dev, rank, world):
         if rank == 0:
             gathered = sum(v.numel() * v.element_size() for v in out.values())
         del out
-    tt = torch.tensor([t1 - t0, t2 - t1, t_gather, fused_s], dtype=torch.float64, device=dev)
+    tt = torch.tensor([t1 - t0, t2 - t1, t_gather, fused_s, gae_kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     shard_bytes = sum(v.numel() * v.element_size() for v in buf.state_dict().values())
     envs.close()
     del buf
     torch.cuda.empty_cache()
+    fused_ms = float(tt[3]) / T * 1e3
     r = {
-        "workload": "BASELINE cfg4: %d envs/GPU x %d GPUs, PPO n_steps=%d, stack=%d, random policy (device "
-                    "Philox; values/log-probs zero: policy network out of scope)" % (n, world, T, args.stack),
+        "workload": "BASELINE cfg4: %d envs/GPU x %d GPUs, PPO n_steps=%d, stack=%d, windowed observations, random "
+                    "policy (device Philox; values/log-probs zero) -- the policy-in-the-loop rate beside it"
+                    % (n, world, T, args.stack),
         "rollout_s": round(float(tt[0]), 4),
         "rollout_env_steps_per_s": round(n * world * T / float(tt[0]), 1),
-        "rollout_kernel": "f16_rollout_kernel (the whole rollout in one launch, state on-chip)",
+        "rollout_kernel": "f16_rollout_kernel (the whole rollout in one launch, state on-chip, windowed output)",
         "rollout_fused_steps_s": round(float(tt[3]), 4),
         "rollout_fused_steps_env_steps_per_s": round(n * world * T / float(tt[3]), 1),
+        "rollout_fused_ms_per_step": round(fused_ms, 5),
+        "window_step_ms_same_envs": round(plain_ms, 5),
+        "fused_over_plain_step": round(fused_ms / plain_ms, 4),
+        **cont,
         "gae_ms": round(float(tt[1]) * 1e3, 3),
+        "gae_kernel_ms": round(float(tt[4]), 4),
+        "gae_achieved_GBps": round(gae_bytes / (float(tt[4]) * 1e-3) / 1e9, 1),
+        "gae_frac_of_hbm_peak": round(gae_bytes / (float(tt[4]) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "gae_bytes": gae_bytes,
+        **pol,
         "shard_bytes_per_rank": shard_bytes,
         "gather_s": round(float(tt[2]), 4) if world > 1 else None,
         "gather_bytes_at_rank0": gathered if world > 1 else None,

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-from .abi import EnvConfig, RolloutSlot
+from .abi import F16ENV_ABI_VERSION, EnvConfig, RolloutSlot
 
 LIB_PATH = os.environ.get("F16ENV_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libf16env.so")
 
@@ -69,6 +69,10 @@ def lib():
     _set(L, "f16env_obs_bounds_count", [vp, vp, ctypes.POINTER(u64)], i32)
     _set(L, "f16env_debug_checks", [vp, vp, ctypes.POINTER(ctypes.c_uint32)], i32)
     L.f16env_rollout_random.argtypes = [vp, vp, u64, u64, i32] + [vp] * 7
+    _set(L, "f16env_window_rollout_random", [vp, vp, u64, u64, i32, i32, i32, i32] + [vp] * 5, i32)
+    _set(L, "f16env_window_step_rollout", [vp, vp, ctypes.POINTER(RolloutSlot), vp, i32, i32], i32)
+    _set(L, "f16env_bootstrap_timeouts", [vp, i64, vp, vp, vp, vp, ctypes.c_double], i32)
+    _set(L, "f16env_abi_version", [], i32)
     L.f16env_set_state.argtypes = [vp, vp, vp]
     L.f16env_trim.argtypes = [vp, vp, vp, vp, vp]
     L.f16env_sample_actions.argtypes = [vp, vp, u64, u64, vp]
@@ -90,8 +94,15 @@ def lib():
     L.f16env_last_error.restype = ctypes.c_char_p
     for name in ("f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_reset",
                  "f16env_step", "f16env_get_state", "f16env_set_state", "f16env_trim",
-                 "f16env_sample_actions", "f16env_gae", "f16env_features"):
+                 "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_rollout_random"):
         getattr(L, name).restype = i32
+    # the header's F16ENV_ABI_VERSION must be the library's (a stale build behind a changed
+    # signature would be called with the wrong arguments); libraries from before the version
+    # export (ABI 2) load only when named explicitly through F16ENV_LIB (tools comparing builds)
+    got = L.f16env_abi_version() if hasattr(L, "f16env_abi_version") else 2
+    if got != F16ENV_ABI_VERSION and (got != 2 or not os.environ.get("F16ENV_LIB")):
+        raise F16EnvError("%s has ABI version %d, this binding expects %d: rebuild it (python -m f16_jsb_amd.build)"
+                          % (LIB_PATH, got, F16ENV_ABI_VERSION))
     _lib = L
     return L
 
@@ -108,7 +119,8 @@ EXPORTED_SYMBOLS = (
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_obs_bounds_count", "f16env_debug_checks", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
     "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order", "f16env_window_clear_fresh",
-    "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt",
+    "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt", "f16env_window_step_rollout",
+    "f16env_window_rollout_random", "f16env_bootstrap_timeouts", "f16env_abi_version",
     "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end", "f16env_profile_times",
     "f16env_algorithmic_bytes_per_env_step", "f16env_last_error",

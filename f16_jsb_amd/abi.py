@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 
-F16ENV_ABI_VERSION = 2
+F16ENV_ABI_VERSION = 3  # include/f16env.h (checked against f16env_abi_version() at load)
 F16_OBS_DIM = 15
 F16_ACT_DIM = 4
 
@@ -138,9 +138,12 @@ def algorithmic_bytes_per_env_step(stack_k: int, state_bytes: int, layout: str =
     return 16 + 60 * stack_k + 60 * (stack_k - 1) + 4 + 2 + 2 * state_bytes
 
 
+F16_SLOT_CLIP = 0x1  # the env steps np.clip(act, low, high); the slot keeps act unclipped
+
+
 class RolloutSlot(ctypes.Structure):
     """f16env_rollout_slot (include/f16env.h): one slot of a device rollout buffer filled by
-    f16env_step_rollout; NULL pointers are not written."""
+    f16env_step_rollout / f16env_window_step_rollout; NULL pointers are not written."""
     _fields_ = [
         ("act_seed", ctypes.c_uint64),
         ("act_step", ctypes.c_uint64),
@@ -149,4 +152,7 @@ class RolloutSlot(ctypes.Structure):
         ("rewards", ctypes.c_void_p),
         ("next_start", ctypes.c_void_p),
         ("features", ctypes.c_void_p),
+        ("next_frame", ctypes.c_void_p),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]

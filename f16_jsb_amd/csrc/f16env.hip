@@ -121,6 +121,20 @@ __device__ __forceinline__ float4 philox_action(uint64_t seed, uint64_t gid, uin
   return v;
 }
 
+// np.clip(actions, action_space.low, action_space.high) (on_policy_algorithm.py:216: SB3 clips
+// the policy's Gaussian sample to the Box before env.step) on float32, as numpy's clip ufunc
+// computes it: min(max(x, lo), hi) with max(a, b) = isnan(a) ? a : (a > b ? a : b) and min
+// likewise with < (numpy/_core/src/umath/clip.cpp _NPY_CLIP): NaN passes through, -0 clips to +0
+// at a 0 bound
+__device__ __forceinline__ float np_clip(float x, float lo, float hi) {
+  const float m = (x != x) ? x : (x > lo ? x : lo);
+  return (m != m) ? m : (m < hi ? m : hi);
+}
+__device__ __forceinline__ float4 clip_box(float4 a) {  // Box [-1,-1,-1,0]..[1,1,1,1] (jsbsim_gym.py:143-148)
+  return make_float4(np_clip(a.x, -1.0f, 1.0f), np_clip(a.y, -1.0f, 1.0f), np_clip(a.z, -1.0f, 1.0f),
+                     np_clip(a.w, 0.0f, 1.0f));
+}
+
 #define FEAT_IN 15
 #define FEAT_OUT 17
 // jsbsim_gym/features.py:37-67 on one frame o[15] -> y[17], float32 with torch's per-op
@@ -533,9 +547,11 @@ struct StepArgs {
   int32_t lds_image;
   // rollout slot (f16env_step_rollout; all NULL / 0 for f16env_step)
   int32_t sample_act;          // act == NULL: draw the actions in-kernel (seed, step)
+  int32_t clip_act;            // F16_SLOT_CLIP: the env steps np.clip(act, low, high), r_act keeps act
   uint64_t act_seed, act_step;
-  float* r_frame;              // N x 15: newest frame of obs_prev
-  float* r_act;                // N x 4: the actions applied
+  float* r_frame;              // N x 15: newest frame of obs_prev (contiguous layout)
+  float* r_next_frame;         // N x 15: newest frame of the returned obs (windowed layout)
+  float* r_act;                // N x 4: the actions (as given: unclipped)
   float* r_rew;                // N: rewards
   float* r_next_start;         // N: done as 0/1 float (episode_starts of the next slot)
   // windowed observations (f16env_step_window): the frame histories of this step (wx, the one
@@ -692,7 +708,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   double ce = 1.0, se = 0.0;
   AltRef A;
   if (live) {
-    const float cmd[4] = {av.x, av.y, av.z, av.w};
+    const float4 ac = (ROLL && a.clip_act) ? clip_box(av) : av;  // the env steps the clipped action
+    const float cmd[4] = {ac.x, ac.y, ac.z, ac.w};
     L.step += 1;                                              // jsbsim_gym.py:215
     if (GUST) {  // cfg5 Gauss-Markov gust update, once per env step before the frames
       float xi[3];
@@ -829,7 +846,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // windowed step resets them itself (in_step_reset)
   const bool autoreset = (!DEFER || in_step_reset) && !(a.E.flags & F16_FLAG_NO_AUTORESET);
   // rollout slot frame = newest frame of obs_prev (what the policy acted on), for every lane
-  if (ROLL && a.r_frame && rows > 0) {
+  // (contiguous layout; the windowed build writes the returned observation's newest frame
+  // below, r_next_frame)
+  if (ROLL && !WIN && a.r_frame && rows > 0) {
     if (image) {
       __builtin_amdgcn_wave_barrier();
       float* dst = a.r_frame + row0 * F16_OBS_DIM;
@@ -897,12 +916,40 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
           const int r = 16 * j + (lane >> 2);
           st16<NT>(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wenv), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
         }
+        if (ROLL && h == 0 && a.r_next_frame) {
+          // the rollout's frame log: the returned observation's newest frame (the next slot's
+          // frame), the wave's 64 rows as 960 contiguous floats = 240 float4 from the same
+          // staging (element c of slot r at float4 r*4 + ((c>>2) ^ sw(r)), component c & 3);
+          // a log whose rows are not 16-B aligned (N % 4 != 0) takes dword stores
+          const float* sf = reinterpret_cast<const float*>(st4);
+          float* dstf = a.r_next_frame + row0 * F16_OBS_DIM;
+          const bool al = ((uintptr_t)dstf & 15) == 0;
+          for (int u = lane; u < 64 * F16_OBS_DIM / 4; u += 64) {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int e = 4 * u + i, r = e / F16_OBS_DIM, c = e - r * F16_OBS_DIM;
+              v[i] = sf[(r * 4 + ((c >> 2) ^ ((r >> 2) & 3))) * 4 + (c & 3)];
+            }
+            if (al) {
+              reinterpret_cast<float4*>(dstf)[u] = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) dstf[4 * u + i] = v[i];
+            }
+          }
+        }
       }
       __builtin_amdgcn_wave_barrier();
     } else if (live) {
       const int64_t off = k * a.wenv + (int64_t)p * a.wrow;
       put_slot<NT>(a.wx + off, reset_now ? f0 : f);
       put_slot<NT>(a.wy + off, f);
+      if (ROLL && a.r_next_frame) {
+        const float* fr = reset_now ? f0 : f;
+#pragma unroll
+        for (int c = 0; c < F16_OBS_DIM; ++c) a.r_next_frame[k * F16_OBS_DIM + c] = fr[c];
+      }
     }
     F16_STAMP(stamps, ST_COPY);
   } else if (image) {
@@ -1054,34 +1101,43 @@ __global__ __launch_bounds__(BLOCK, 1) void f16_step_gt_kernel(STEP_PRE_ARGS, St
 }
 // windowed-observation build (f16env_step_window): no stack image, LDS holds the tables and
 // the per-wave frame staging
-template <int MODE, int OCC>
+// ROLL: the rollout-slot build (f16env_window_step_rollout: in-kernel Philox or clipped policy
+// actions, the slot's actions / rewards / next starts and the returned observation's newest
+// frame); the plain windowed step carries none of its code.
+template <int MODE, int OCC, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_kernel(const float4* __restrict__ sc, const float* __restrict__ act,
                                                                   const float4* __restrict__ tmpl, int64_t n, StepArgs a) {
   STEP_SHARED
   const StepPre pre = {sc, act, tmpl, n};
-  step_body<MODE, false, false, OCC == 2, true>(a, sT, sTmpl, sDone, dynl, &pre);
+  step_body<MODE, false, ROLL, OCC == 2, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 // ... with non-temporal state and frame-slot stores, for grids resident in one round (st16)
-template <int MODE, int OCC>
+template <int MODE, int OCC, bool ROLL = false>
 __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(const float4* __restrict__ sc,
                                                                      const float* __restrict__ act,
                                                                      const float4* __restrict__ tmpl, int64_t n,
                                                                      StepArgs a) {
   STEP_SHARED
   const StepPre pre = {sc, act, tmpl, n};
-  step_body<MODE, false, false, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
+  step_body<MODE, false, ROLL, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 using StepKernel = void (*)(const float4*, const float*, const float4*, int64_t, StepArgs);
 using WinKernel = StepKernel;
-static WinKernel step_win_kernel_for(int mode, int occ, int nt) {
+template <bool ROLL>
+static WinKernel step_win_kernel_for_r(int mode, int occ, int nt) {
   static const WinKernel table[2][2][4] = {
-      {{f16_step_win_kernel<0, 1>, f16_step_win_kernel<1, 1>, f16_step_win_kernel<2, 1>, f16_step_win_kernel<3, 1>},
-       {f16_step_win_kernel<0, 2>, f16_step_win_kernel<1, 2>, f16_step_win_kernel<2, 2>, f16_step_win_kernel<3, 2>}},
-      {{f16_step_win_nt_kernel<0, 1>, f16_step_win_nt_kernel<1, 1>, f16_step_win_nt_kernel<2, 1>,
-        f16_step_win_nt_kernel<3, 1>},
-       {f16_step_win_nt_kernel<0, 2>, f16_step_win_nt_kernel<1, 2>, f16_step_win_nt_kernel<2, 2>,
-        f16_step_win_nt_kernel<3, 2>}}};
+      {{f16_step_win_kernel<0, 1, ROLL>, f16_step_win_kernel<1, 1, ROLL>, f16_step_win_kernel<2, 1, ROLL>,
+        f16_step_win_kernel<3, 1, ROLL>},
+       {f16_step_win_kernel<0, 2, ROLL>, f16_step_win_kernel<1, 2, ROLL>, f16_step_win_kernel<2, 2, ROLL>,
+        f16_step_win_kernel<3, 2, ROLL>}},
+      {{f16_step_win_nt_kernel<0, 1, ROLL>, f16_step_win_nt_kernel<1, 1, ROLL>, f16_step_win_nt_kernel<2, 1, ROLL>,
+        f16_step_win_nt_kernel<3, 1, ROLL>},
+       {f16_step_win_nt_kernel<0, 2, ROLL>, f16_step_win_nt_kernel<1, 2, ROLL>, f16_step_win_nt_kernel<2, 2, ROLL>,
+        f16_step_win_nt_kernel<3, 2, ROLL>}}};
   return table[nt ? 1 : 0][occ == 2 ? 1 : 0][mode & 3];
+}
+static WinKernel step_win_kernel_for(int mode, int occ, int nt, bool roll = false) {
+  return roll ? step_win_kernel_for_r<true>(mode, occ, nt) : step_win_kernel_for_r<false>(mode, occ, nt);
 }
 static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WIN_WAVE_FLOATS;
 // variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
@@ -1101,127 +1157,200 @@ static StepKernel step_kernel_for(int mode, int variant, bool roll = false) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Persistent rollout under the uniform random policy (f16env_rollout_random): T env steps of
-// every lane in ONE launch. The actions come from the f16env_sample_actions Philox stream, so
-// no step waits for a host or a policy: each lane keeps its state in registers and its last K
-// frames in an LDS ring across the whole rollout, and per step writes only the rollout slot
-// (newest frame of the observation acted on, action, reward, next episode start). State and
-// the final observation stack are stored once, at the end. Same arithmetic, RNG streams and
-// auto-reset as T launches of the fused step (f16env_step_rollout): bit-identical results
-// (build.py -ffp-contract=on: contraction is fixed per source expression, not per kernel).
+// Persistent rollout under the uniform random policy (f16env_rollout_random /
+// f16env_window_rollout_random): T env steps of every lane in ONE launch. The actions come from
+// the f16env_sample_actions Philox stream, so no step waits for a host or a policy: each lane
+// keeps its state in registers across the whole rollout and per step writes only the rollout
+// slot -- the action, reward and next episode start of step t, and the newest frame of the
+// observation it returns, which is the frame slot t + 1 acts on (frames[0] is the newest frame
+// of the observation before step 0). No frame stack is kept on chip: the final observation is
+// rebuilt at the end from the frame log the lane wrote (obs[j] = F[max(T-K+1+j, s)], s the
+// lane's last episode start, F[T] the last frame in registers, F[t <= 0] from the observation
+// before the rollout -- rollout.py rebuild_observations), so K is not bounded by LDS (round 3's
+// ring held K <= 8 frames per lane). cfg5 modes (MODE != 0): gusts per step as the step kernel,
+// and a finished lane resets from the reset cache when it holds its next episode's row (the
+// first reset of a lane in the rollout; f16_ic_fill_kernel fills it before the launch), else
+// by its own RunIC. Same arithmetic, RNG streams and auto-reset as T launches of the fused step
+// (f16env_step_rollout / f16env_window_step_rollout): bit-identical results (build.py
+// -ffp-contract=on: contraction is fixed per source expression, not per kernel).
 // ------------------------------------------------------------------------------------------
 struct RollArgs {
-  SoA s, tmpl;
-  const float* obs_prev;  // N x K x 15 before step 0
-  float* obs;             // N x K x 15 after step T-1
-  float* frames;          // T x N x 15
+  SoA s, tmpl, icc;       // icc: cfg5 reset cache (MODE != 0; c == nullptr: every reset a RunIC)
+  // the observation before step 0: frame j of lane k at obs_prev + k * in_row + j * in_pitch
+  // (contiguous N x K x 15: K*15, 15; a position-major window: 16, N*16)
+  const float* obs_prev;
+  int64_t in_row, in_pitch;
+  // the observation after step T-1, written the same way to out0 and (when not NULL) out1 --
+  // the two window histories -- with out_slot floats per frame (15, or 16: a 64-B slot)
+  float* out0;
+  float* out1;
+  int64_t out_row, out_pitch;
+  int32_t out_slot;
+  float* frames;          // T x N x 15: frames[t] = newest frame of the observation step t acts on
   float* actions;         // T x N x 4
   float* rewards;         // T x N
   float* next_start;      // (T - 1) x N: 1.0 where the lane finished at step t < T-1
   float* last_start;      // N: the same for step T-1
-  unsigned long long* nonfinite;  // F16_FLAG_NAN_GUARD quarantine count
+  unsigned long long* nonfinite;  // [0] F16_FLAG_NAN_GUARD quarantines, [2] F16_FLAG_OBS_CHECK
   uint64_t seed, step0;
   int32_t T;
+  int32_t clear_fresh;    // both output windows are whole: no lane needs a FRESH fill next step
   EnvArgs E;
   ModelConsts C;
 };
-static constexpr int RING_PITCH = 16;  // floats per ring frame slot (15 used)
-__global__ __launch_bounds__(BLOCK, 1) void f16_rollout_kernel(RollArgs a) {
+template <int MODE, int OCC>
+__global__ __launch_bounds__(BLOCK, OCC) void f16_rollout_kernel(RollArgs a) {
   __shared__ __align__(16) float sT[F16_BLOB_FLOATS];
   __shared__ __align__(16) float4 sTmpl[NCOL + TMPL_FRAME_COLS];
-  extern __shared__ __align__(16) float ring[];  // [K][BLOCK][RING_PITCH]
+  __shared__ __align__(16) float4 sF[BLOCK * 4];  // per wave: its 64 new frames as [64][4] float4
+  constexpr bool GUST = (MODE & 2) != 0;
   const int K = a.E.K, tid = threadIdx.x;
   const int64_t k = (int64_t)blockIdx.x * BLOCK + tid;
-  const bool live = k < a.E.n;
+  const int64_t N = a.E.n;
+  const bool live = k < N;
   stage_tables_issue(sT);
-  if (tid < NCOL + TMPL_FRAME_COLS)
+  if (MODE == 0 && tid < NCOL + TMPL_FRAME_COLS)
     dma16(reinterpret_cast<const float*>(a.tmpl.c + (tid < NCOL ? tid : tid + NCOL_ALL - NCOL)),
           reinterpret_cast<float*>(sTmpl));
   Lane L;
-  if (live) lane_load(a.s, k, L);
+  float fn[F16_OBS_DIM];  // newest frame of the lane's current observation
+  if (live) {
+    lane_load<GUST>(a.s, k, L);
+    const float* op = a.obs_prev + k * a.in_row + (int64_t)(K - 1) * a.in_pitch;
+#pragma unroll
+    for (int c = 0; c < F16_OBS_DIM; ++c) fn[c] = op[c];
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (!live) return;  // no barrier below
-  float* my = ring + (size_t)tid * RING_PITCH;
-  const size_t slot_stride = (size_t)BLOCK * RING_PITCH;
-  {
-    const float* op = a.obs_prev + k * (int64_t)K * F16_OBS_DIM;
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-      for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = op[j * F16_OBS_DIM + c];
-  }
-  // head: ring slot of the oldest frame, the same for every lane (a reset rewrites all K slots
-  // and advances it like an append), so the newest frame of the observation an action acts on
-  // -- the rollout slot's frame -- sits in one uniform slot for the whole wave
-  int head = 0;
-  const int64_t N = a.E.n;
   const int wave = tid >> 6, lane = tid & 63;
   const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
-  // a full wave writes its 64 frames (3 840 contiguous bytes) as 240 float4 gathered from the
-  // ring, instead of fifteen 4-byte stores per lane at a 60-byte stride
-  const bool coalesced = a.E.n - row0 >= 64 && (N * F16_OBS_DIM) % 4 == 0 && ((uintptr_t)a.frames & 15) == 0;
+  // a full wave writes its 64 frames (3 840 contiguous bytes) as 240 float4 gathered from its
+  // LDS staging, instead of fifteen 4-byte stores per lane at a 60-byte stride
+  const bool coalesced = N - row0 >= 64 && (N * F16_OBS_DIM) % 4 == 0 && ((uintptr_t)a.frames & 15) == 0;
+  float4* stg = sF + wave * 256;
+  auto put_frame = [&](int64_t t) {  // frames[t] = fn for every lane of the wave
+    if (coalesced) {
+      __builtin_amdgcn_wave_barrier();
+      stg[lane * 4 + 0] = make_float4(fn[0], fn[1], fn[2], fn[3]);
+      stg[lane * 4 + 1] = make_float4(fn[4], fn[5], fn[6], fn[7]);
+      stg[lane * 4 + 2] = make_float4(fn[8], fn[9], fn[10], fn[11]);
+      stg[lane * 4 + 3] = make_float4(fn[12], fn[13], fn[14], 0.0f);
+      __builtin_amdgcn_wave_barrier();
+      const float* src = reinterpret_cast<const float*>(stg);
+      float4* dst = reinterpret_cast<float4*>(a.frames + (t * N + row0) * F16_OBS_DIM);
+      for (int q = lane; q < 64 * F16_OBS_DIM / 4; q += 64) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * q + i, r = e / F16_OBS_DIM;
+          v[i] = src[r * 16 + (e - r * F16_OBS_DIM)];
+        }
+        dst[q] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+      float* fr = a.frames + (t * N + k) * F16_OBS_DIM;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) fr[c] = fn[c];
+    }
+  };
+  put_frame(0);
   const uint64_t gid = (uint64_t)(a.E.id_base + k);
+  int last_s = -(1 << 30);  // index t of the lane's last reset frame F[t] in this rollout (none yet)
+  bool cache_fresh = a.icc.c != nullptr;  // the cached row can only serve the lane's first reset
   for (int t = 0; t < a.T; ++t) {
     const float4 av = philox_action(a.seed, gid, a.step0 + (uint64_t)t);
     const float cmd[4] = {av.x, av.y, av.z, av.w};
     L.step += 1;  L.flags &= ~LANE_FLAG_FRESH;                                              // jsbsim_gym.py:215
+    if (GUST) {  // cfg5 Gauss-Markov gust update, once per env step before the frames (as step_body)
+      float xi[3];
+      rng_normals(a.E.seed, gid, (uint32_t)(L.ep_count - 1), (uint32_t)L.step, xi);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        L.gust[j] = __builtin_fmaf(a.E.gust_a, L.gust[j], a.E.gust_b * xi[j]);
+        L.wind[j] = L.wst[j] + L.gust[j];
+      }
+    }
     double ce, se;
     earth_angle(L.epa, ce, se);
     const AltRef A = alt_ref(L, ce, se);
 #ifdef F16_STAMPS
     Stamps stamps = {};
 #endif
-    for (int s = 0; s < a.E.down_sample; ++s) frame<false, false>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
+    for (int s = 0; s < a.E.down_sample; ++s)
+      frame<OCC == 2, GUST>(L, cmd, ce, se, A, sT, a.C, false F16_STAMP_PASS);  // :225-232
     float f[F16_OBS_DIM];
     make_frame(L, ce, se, A, f);                              // :234
     float r32;
     const int fl = env_reward(L, f, a.E, r32);
     const int done = fl & 3;
-    if (fl & 4) atomicAdd(a.nonfinite, 1ull);  // rare: one lane at a time
-    const int64_t row = (int64_t)t * N + k;
-    const int nslot = head == 0 ? K - 1 : head - 1;  // newest frame
-    F16_CHECK(head >= 0 && head < K && nslot >= 0 && nslot < K, DBG_RING_SLOT);
-    if (coalesced) {
-      __builtin_amdgcn_wave_barrier();
-      const float* src = ring + nslot * slot_stride + (size_t)(wave * 64) * RING_PITCH;
-      float4* dst = reinterpret_cast<float4*>(a.frames + ((int64_t)t * N + row0) * F16_OBS_DIM);
-      for (int q = lane; q < 64 * F16_OBS_DIM / 4; q += 64) {
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int e = 4 * q + i, r = e / F16_OBS_DIM;
-          v[i] = src[r * RING_PITCH + (e - r * F16_OBS_DIM)];
-        }
-        dst[q] = make_float4(v[0], v[1], v[2], v[3]);
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else {
-      float* fr = a.frames + row * F16_OBS_DIM;
-#pragma unroll
-      for (int c = 0; c < F16_OBS_DIM; ++c) fr[c] = my[nslot * slot_stride + c];
+    if (a.E.flags & F16_FLAG_NAN_GUARD) {
+      const unsigned long long qm = __ballot(fl & 4);
+      if (qm && lane == 0) atomicAdd(a.nonfinite, (unsigned long long)__popcll(qm));
     }
+    if (a.E.flags & F16_FLAG_OBS_CHECK) {  // jsbsim_gym.py:268-285 on the new frame
+      const unsigned long long om = __ballot(obs_out_of_bounds(f));
+      if (om && lane == 0) atomicAdd(a.nonfinite + 2, (unsigned long long)__popcll(om));
+    }
+    const int64_t row = (int64_t)t * N + k;
     reinterpret_cast<float4*>(a.actions)[row] = av;
     a.rewards[row] = r32;
     if (t + 1 < a.T) a.next_start[row] = done ? 1.0f : 0.0f;
     else a.last_start[k] = done ? 1.0f : 0.0f;
     if (done) {  // dummy_vec_env.py:68-71: the next observation is K x the reset frame
-      float f0[F16_OBS_DIM];
-      lane_reset_template(L, sTmpl, a.E, k, f0);
-      for (int j = 0; j < K; ++j)
+      if (MODE == 0) {
+        lane_reset_template(L, sTmpl, a.E, k, fn);
+      } else if (cache_fresh && __float_as_int(a.icc.c[(int64_t)15 * a.icc.n + k].w) == L.ep_count + 1) {
+        lane_load<GUST>(a.icc, k, L);  // the lane's next reset, evaluated ahead (f16_ic_fill_kernel)
 #pragma unroll
-        for (int c = 0; c < F16_OBS_DIM; ++c) my[j * slot_stride + c] = f0[c];
-    } else {  // deque append (:235): the oldest frame's slot takes the new one
+        for (int j = 0; j < TMPL_FRAME_COLS; ++j) {
+          const float4 v = a.icc.c[(int64_t)(NCOL_ALL + j) * a.icc.n + k];
+          fn[4 * j] = v.x; fn[4 * j + 1] = v.y; fn[4 * j + 2] = v.z; fn[4 * j + 3] = v.w;
+        }
+        fn[12] = L.goal[0]; fn[13] = L.goal[1]; fn[14] = L.goal[2];
+        cache_fresh = false;
+      } else {
+        lane_reset_mode<MODE>(L, a.E, k, sT, a.C, fn);
+        cache_fresh = false;
+      }
+      last_s = t + 1;
+    } else {
 #pragma unroll
-      for (int c = 0; c < F16_OBS_DIM; ++c) my[head * slot_stride + c] = f[c];
+      for (int c = 0; c < F16_OBS_DIM; ++c) fn[c] = f[c];
     }
-    head = (head + 1 == K) ? 0 : head + 1;
+    if (t + 1 < a.T) put_frame(t + 1);
   }
-  lane_store(a.s, k, L);
-  float* o = a.obs + k * (int64_t)K * F16_OBS_DIM;
+  if (a.clear_fresh) L.flags &= ~LANE_FLAG_FRESH;
+  lane_store<GUST>(a.s, k, L);
+  // the final observation, oldest frame first: F[max(T-K+1+j, last_s)]; F[T] = fn, F[1..T-1] from
+  // this wave's own frame-log rows (made visible to the reads by the fence), F[t <= 0] from the
+  // observation before the rollout (F[0] is also frames[0])
+  __threadfence();
+  const int T = a.T;
   for (int j = 0; j < K; ++j) {
-    const int sl = (head + j) % K;
+    const int idx = max(T - K + 1 + j, last_s);
+    float v[F16_OBS_DIM];
+    if (idx == T) {
 #pragma unroll
-    for (int c = 0; c < F16_OBS_DIM; ++c) o[j * F16_OBS_DIM + c] = my[sl * slot_stride + c];
+      for (int c = 0; c < F16_OBS_DIM; ++c) v[c] = fn[c];
+    } else if (idx >= 1) {
+      const float* src = a.frames + ((int64_t)idx * N + k) * F16_OBS_DIM;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) v[c] = __builtin_nontemporal_load(src + c);
+    } else {
+      const float* src = a.obs_prev + k * a.in_row + (int64_t)(idx + K - 1) * a.in_pitch;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) v[c] = src[c];
+    }
+    F16_CHECK(idx >= 1 - K && idx <= T, DBG_RING_SLOT);
+    for (int b = 0; b < 2; ++b) {
+      float* o = (b == 0 ? a.out0 : a.out1);
+      if (!o) continue;
+      o += k * a.out_row + (int64_t)j * a.out_pitch;
+#pragma unroll
+      for (int c = 0; c < F16_OBS_DIM; ++c) o[c] = v[c];
+      if (a.out_slot > F16_OBS_DIM) o[F16_OBS_DIM] = 0.0f;
+    }
   }
 }
 
@@ -1561,27 +1690,68 @@ __global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t s
 // compute_returns_and_advantage) with numpy's float32 per-operation rounding: every product
 // and sum is rounded separately (no FMA), gamma and gamma*lambda are rounded to float32
 // exactly as numpy casts a Python float against a float32 array.
-__global__ void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __restrict__ rewards,
-                               const float* __restrict__ values, const float* __restrict__ ep_starts,
-                               const float* __restrict__ last_values, const uint8_t* __restrict__ dones,
-                               float g, float gl, float* __restrict__ adv, float* __restrict__ ret) {
+// The recurrence is serial per env (bit-exactness forbids reassociating it into a scan), and at
+// cfg4's 32 768 envs one lane per env is only 512 waves, each walking 2 048 steps. Its loads do
+// not depend on the chain, so they are software-pipelined: the rewards / values / starts of the
+// next block of U steps are issued before the current block is computed, keeping ~2U steps of
+// loads in flight per lane (round 3's loop waited on each step's three loads in turn: 0.13 of
+// HBM peak). LPW lanes of each 64-lane wave carry an env (LPW = 32: 1 024 half-populated waves
+// at 32 768 envs, one per SIMD, twice the memory requests in flight for the same bytes).
+// Streaming data: non-temporal loads and stores.
+template <int U>
+__device__ __forceinline__ void gae_load(int64_t s0, int64_t n_envs, int64_t e, const float* __restrict__ rewards,
+                                         const float* __restrict__ values, const float* __restrict__ ep_starts,
+                                         float (&r)[U], float (&v)[U], float (&st)[U]) {
+#pragma unroll
+  for (int i = 0; i < U; ++i) {
+    const int64_t idx = (s0 + i) * n_envs + e;
+    r[i] = __builtin_nontemporal_load(rewards + idx);
+    v[i] = __builtin_nontemporal_load(values + idx);
+    st[i] = __builtin_nontemporal_load(ep_starts + idx);
+  }
+}
+template <int U, int LPW>
+__global__ __launch_bounds__(64) void f16_gae_kernel(int64_t n_steps, int64_t n_envs, const float* __restrict__ rewards,
+                                                     const float* __restrict__ values, const float* __restrict__ ep_starts,
+                                                     const float* __restrict__ last_values, const uint8_t* __restrict__ dones,
+                                                     float g, float gl, float* __restrict__ adv, float* __restrict__ ret) {
   // float32 per-op rounding as numpy (no FMA contraction; __f*_rn still contract under -O3)
 #pragma clang fp contract(off)
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)threadIdx.x >= LPW) return;
+  const int64_t e = (int64_t)blockIdx.x * LPW + threadIdx.x;
   if (e >= n_envs) return;
   float lgl = 0.0f;
   float nv = last_values[e];
   float nnt = 1.0f - (dones[e] ? 1.0f : 0.0f);
-  for (int64_t s = n_steps - 1; s >= 0; --s) {
+  // one backward step of buffers.py:425-436 at step s
+  auto step = [&](int64_t s, float r, float v, float st) {
+#pragma clang fp contract(off)
     const int64_t i = s * n_envs + e;
-    const float v = values[i];
     const float t2 = (g * nv) * nnt;
-    const float delta = (rewards[i] + t2) - v;
+    const float delta = (r + t2) - v;
     lgl = delta + (gl * nnt) * lgl;
-    adv[i] = lgl;
-    ret[i] = lgl + v;
+    __builtin_nontemporal_store(lgl, adv + i);
+    __builtin_nontemporal_store(lgl + v, ret + i);
     nv = v;
-    nnt = 1.0f - ep_starts[i];
+    nnt = 1.0f - st;
+  };
+  const int64_t nb = n_steps / U;  // whole blocks [b U, b U + U); the n_steps % U last steps first
+  for (int64_t s = n_steps - 1; s >= nb * U; --s) {
+    const int64_t i = s * n_envs + e;
+    step(s, rewards[i], values[i], ep_starts[i]);
+  }
+  if (nb == 0) return;
+  float r0[U], v0[U], s0[U];
+  gae_load<U>((nb - 1) * U, n_envs, e, rewards, values, ep_starts, r0, v0, s0);
+  for (int64_t b = nb - 1; b >= 0; --b) {
+    float r1[U], v1[U], s1[U];
+    if (b > 0) gae_load<U>((b - 1) * U, n_envs, e, rewards, values, ep_starts, r1, v1, s1);  // next block in flight
+#pragma unroll
+    for (int i = U - 1; i >= 0; --i) step(b * U + i, r0[i], v0[i], s0[i]);
+    if (b > 0) {
+#pragma unroll
+      for (int i = 0; i < U; ++i) { r0[i] = r1[i]; v0[i] = v1[i]; s0[i] = s1[i]; }
+    }
   }
 }
 
@@ -1729,8 +1899,9 @@ struct f16env {
     int32_t* ep_len;
   } wb;
   SoA soa, tmpl;
-  // cfg5 modes, windowed layout: reset cache (f16_ic_fill_kernel), allocated at the first
-  // windowed step; refilled every icc_period windowed steps
+  // cfg5 modes: reset cache (f16_ic_fill_kernel), allocated at create (or at the first use by a
+  // handle that gained wind later); refilled every icc_period windowed steps, and at the next
+  // one after anything that changes the lanes' episode counters (icc_steps = 0)
   SoA icc;
   int64_t icc_steps;
   int icc_period;
@@ -1924,10 +2095,18 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
       }
     }
   }
-  if (cfg->stack_k <= 8 &&
-      hipFuncSetAttribute((const void*)f16_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)(sizeof(float) * cfg->stack_k * BLOCK * RING_PITCH)) != hipSuccess)
-    (void)hipGetLastError();  // f16env_rollout_random reports it
+  // cfg5 modes: the reset cache up front (its bytes are part of f16env_state_bytes); a handle
+  // that only gains wind later (set_state / a per-lane IC) allocates it at its first use
+  if (h->mode && !(cfg->flags & F16_FLAG_NO_AUTORESET)) {
+    const size_t b = (size_t)ICC_COLS * 16 * (size_t)cfg->n_envs;
+    if (hipMalloc((void**)&h->icc.c, b) != hipSuccess) {
+      h->icc.c = nullptr;
+      hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); hipFree(h->nonfinite); delete h;
+      return set_err(-3, "hipMalloc(reset cache) failed");
+    }
+    hipMemset(h->icc.c, 0, b);  // tag 0: no row valid yet
+    h->bytes += b;
+  }
   hipMemcpy(h->ic_dev, cfg->ic, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + F16_IC_N, cfg->ic_lo, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
   hipMemcpy(h->ic_dev + 2 * F16_IC_N, cfg->ic_hi, sizeof(double) * F16_IC_N, hipMemcpyHostToDevice);
@@ -1935,7 +2114,9 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
   e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) {
-    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); hipFree(h->nonfinite); delete h;
+    hipFree(h->mem); hipFree(h->tmem); hipFree(h->ic_dev); hipFree(h->done_buf); hipFree(h->nonfinite);
+    if (h->icc.c) hipFree(h->icc.c);
+    delete h;
     return set_err(-2, hipGetErrorString(e));
   }
   *out = h;
@@ -2011,6 +2192,7 @@ static inline unsigned nblocks(int64_t n) { return (unsigned)((n + BLOCK - 1) / 
 // then the handle reads back (waits for the stream) whether any lane got some, and switches to
 // the wind kernels if so (the caller's IC is not hot-path).
 static int reset_launch(f16env_t h, hipStream_t st, ResetArgs& a) {
+  h->icc_steps = 0;  // the lanes' episode counters move: the next windowed step refills the reset cache
   a.wind_any = nullptr;
   if (a.ic && !(h->mode & 2)) {
     a.wind_any = reinterpret_cast<int*>(h->nonfinite + 1);
@@ -2071,12 +2253,17 @@ static int step_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, 
   a.done_idx = done_idx; a.n_done = n_done;
   a.nonfinite = h->nonfinite;
   a.sample_act = act ? 0 : 1;
+  a.clip_act = (slot && (slot->flags & F16_SLOT_CLIP)) ? 1 : 0;
   a.act_seed = slot ? slot->act_seed : 0; a.act_step = slot ? slot->act_step : 0;
   a.r_frame = slot ? slot->frame : nullptr;
+  a.r_next_frame = nullptr;
   a.r_act = slot ? slot->actions : nullptr;
   a.r_rew = slot ? slot->rewards : nullptr;
   a.r_next_start = slot ? slot->next_start : nullptr;
   float* feat = slot ? slot->features : nullptr;
+  if (slot && slot->next_frame)
+    return set_err(-1, "rollout slot next_frame is the windowed layout's (f16env_window_step_rollout); "
+                       "the contiguous layout writes frame");
   if ((a.r_frame && ((uintptr_t)a.r_frame & 15) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
     return set_err(-1, "rollout slot frame/actions must be 16-byte aligned");
   a.wx = a.wy = nullptr; a.wrow = a.wenv = 0; a.wpos = 0;
@@ -2137,6 +2324,29 @@ int f16env_set_window_order(f16env_t h, int env_major) {
   return 0;
 }
 
+// cfg5 modes: the reset cache, allocated if this handle has none yet (it gained wind after
+// create), refilled now if `fill` (f16_ic_fill_kernel: every lane whose cached row is not its
+// next episode's)
+static int icc_prepare(f16env_t h, hipStream_t st, bool fill) {
+  const int64_t n = h->cfg.n_envs;
+  if (!h->icc.c) {
+    const size_t b = (size_t)ICC_COLS * 16 * (size_t)n;
+    if (hipMalloc((void**)&h->icc.c, b) != hipSuccess) { h->icc.c = nullptr; return set_err(-3, "hipMalloc(reset cache) failed"); }
+    HIPCHK(hipMemsetAsync(h->icc.c, 0, b, st));  // tag 0: no row valid yet
+    h->bytes += b;
+    fill = true;
+  }
+  h->icc.n = n;
+  if (fill) {
+    using FillKernel = void (*)(SoA, SoA, EnvArgs, ModelConsts);
+    static const FillKernel fills[4] = {f16_ic_fill_kernel<0>, f16_ic_fill_kernel<1>, f16_ic_fill_kernel<2>,
+                                        f16_ic_fill_kernel<3>};
+    hipLaunchKernelGGL(fills[h->mode & 3], dim3(nblocks(n)), dim3(BLOCK), 0, st, h->soa, h->icc, env_args(h), h->C);
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
 static int window_check(f16env_t h, const float* hist_cur, const float* hist_other, int64_t T, int32_t pos) {
   const int K = h->cfg.stack_k;
   if (!hist_cur || (hist_other == nullptr && hist_cur == nullptr)) return set_err(-1, "null history");
@@ -2147,22 +2357,37 @@ static int window_check(f16env_t h, const float* hist_cur, const float* hist_oth
   return 0;
 }
 
-int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_cur, float* hist_other, int64_t T,
-                       int32_t pos, float* rew, uint8_t* terminated, uint8_t* truncated, double* ep_return,
-                       int32_t* ep_len, int32_t* done_idx, int32_t* n_done) {
+static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                            float* hist_cur, float* hist_other, int64_t T, int32_t pos, float* rew,
+                            uint8_t* terminated, uint8_t* truncated, double* ep_return, int32_t* ep_len,
+                            int32_t* done_idx, int32_t* n_done) {
   if (!h) return set_err(-1, "null handle");
-  if (!act || !hist_other || !rew || !terminated || !truncated)
-    return set_err(-1, "act/hist_cur/hist_other/rew/terminated/truncated are required");
+  if ((!act && !slot) || !hist_other || !rew || !terminated || !truncated)
+    return set_err(-1, "act (or a rollout slot)/hist_cur/hist_other/rew/terminated/truncated are required");
   if (int e = window_check(h, hist_cur, hist_other, T, pos)) return e;
   if (hist_cur == hist_other) return set_err(-1, "the two histories must be distinct buffers");
   if (done_idx && !n_done) return set_err(-1, "done_idx requires n_done");
-  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  if (act && ((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
   StepArgs a;
   memset(&a, 0, sizeof a);
   a.s = h->soa; a.tmpl = h->tmpl; a.act = act; a.rew = rew;
   a.term = terminated; a.trunc = truncated; a.ep_ret = ep_return; a.ep_len = ep_len;
   a.done_idx = done_idx; a.n_done = n_done;
   a.nonfinite = h->nonfinite;
+  float* feat = nullptr;
+  if (slot) {
+    if (slot->frame)
+      return set_err(-1, "rollout slot frame is the contiguous layout's; the windowed layout writes next_frame "
+                         "(the newest frame of the returned observation)");
+    a.sample_act = act ? 0 : 1;
+    a.clip_act = (slot->flags & F16_SLOT_CLIP) ? 1 : 0;
+    a.act_seed = slot->act_seed; a.act_step = slot->act_step;
+    a.r_next_frame = slot->next_frame; a.r_act = slot->actions; a.r_rew = slot->rewards;
+    a.r_next_start = slot->next_start;
+    feat = slot->features;
+    if ((a.r_next_frame && ((uintptr_t)a.r_next_frame & 3) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
+      return set_err(-1, "rollout slot next_frame must be 4-byte and actions 16-byte aligned");
+  }
   int64_t P, Q;  // floats between positions, between envs
   window_strides(h, T, P, Q);
   a.wx = hist_cur; a.wy = hist_other; a.wrow = P; a.wenv = Q; a.wpos = pos;
@@ -2177,35 +2402,23 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
   const bool cache = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period > 0;
   a.icc.c = nullptr; a.icc.n = a.E.n;
   if (cache) {
-    if (!h->icc.c) {
-      const size_t b = (size_t)ICC_COLS * 16 * (size_t)a.E.n;
-      if (hipMalloc((void**)&h->icc.c, b) != hipSuccess) { h->icc.c = nullptr; return set_err(-3, "hipMalloc(reset cache) failed"); }
-      HIPCHK(hipMemsetAsync(h->icc.c, 0, b, st));  // tag 0: no row valid yet
-      h->icc_steps = 0;
-    }
-    if (h->icc_steps % h->icc_period == 0) {
-      using FillKernel = void (*)(SoA, SoA, EnvArgs, ModelConsts);
-      static const FillKernel fill[4] = {f16_ic_fill_kernel<0>, f16_ic_fill_kernel<1>, f16_ic_fill_kernel<2>,
-                                         f16_ic_fill_kernel<3>};
-      hipLaunchKernelGGL(fill[h->mode & 3], grid, blk, 0, st, h->soa, h->icc, a.E, h->C);
-      HIPCHK(hipGetLastError());
-    }
+    if (int e = icc_prepare(h, st, h->icc_steps % h->icc_period == 0)) return e;
     ++h->icc_steps;
     a.icc = h->icc;
     if (n_done) HIPCHK(hipMemsetAsync(n_done, 0, sizeof(int32_t), st));  // the caller's done list only
   } else if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) {
     return e;
   }
-  const WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt);
+  const WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt, slot != nullptr);
   const float4* sc = a.s.c;
   const float4* tc = a.tmpl.c;
   const int64_t n = a.E.n;
   if (h->prof_next < (int)h->prof_ev.size() / 2) {
     const int i = h->prof_next++;
     hipExtLaunchKernelGGL(kern, grid, blk, (std::uint32_t)WIN_DYN_LDS, st, h->prof_ev[2 * i], h->prof_ev[2 * i + 1], 0u,
-                          sc, act, tc, n, a);
+                          sc, a.act, tc, n, a);
   } else {
-    hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, sc, act, tc, n, a);
+    hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, sc, a.act, tc, n, a);
   }
   HIPCHK(hipGetLastError());
   if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && !cache) {
@@ -2217,8 +2430,24 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
     HIPCHK(hipGetLastError());
+    if (slot && (slot->next_frame || feat))
+      return set_err(-1, "the deferred-reset windowed step (F16ENV_ICC_PERIOD=0) writes no next_frame / features");
+  }
+  if (feat) {  // policy features of the returned observation, read in place from the window
+    const int64_t blocks = ((int64_t)a.E.n * a.E.K + 255) / 256;
+    hipLaunchKernelGGL(f16_features_strided_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (int64_t)a.E.n,
+                       (int32_t)a.E.K, (const float*)(hist_cur + (int64_t)(pos - a.E.K + 1) * P), Q, P, feat);
+    HIPCHK(hipGetLastError());
   }
   return 0;
+}
+
+int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_cur, float* hist_other, int64_t T,
+                       int32_t pos, float* rew, uint8_t* terminated, uint8_t* truncated, double* ep_return,
+                       int32_t* ep_len, int32_t* done_idx, int32_t* n_done) {
+  if (!act) return set_err(-1, "act is required");
+  return step_window_impl(h, stream, nullptr, act, hist_cur, hist_other, T, pos, rew, terminated, truncated,
+                          ep_return, ep_len, done_idx, n_done);
 }
 
 int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float* rew, uint8_t* terminated,
@@ -2239,6 +2468,16 @@ int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t
   const int b = parity & 1;
   return f16env_step_window(h, stream, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew, h->wb.term,
                             h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr);
+}
+
+int f16env_window_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                               int32_t parity, int32_t pos) {
+  if (!h) return set_err(-1, "null handle");
+  if (!slot) return set_err(-1, "null rollout slot");
+  if (!h->wb.hist[0]) return set_err(-1, "f16env_window_bind first");
+  const int b = parity & 1;
+  return step_window_impl(h, stream, slot, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew,
+                          h->wb.term, h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr);
 }
 
 int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
@@ -2318,28 +2557,102 @@ int f16env_obs_bounds_count(f16env_t h, void* stream, uint64_t* count) {
   return 0;
 }
 
+// persistent rollout launch shared by the contiguous and windowed entry points
+static int rollout_launch(f16env_t h, hipStream_t st, RollArgs& a) {
+  if (a.T < 1) return set_err(-1, "T must be >= 1");
+  if (!a.frames || !a.actions || !a.rewards || !a.last_start || (a.T > 1 && !a.next_start))
+    return set_err(-1, "frames/actions/rewards/last_start (and next_start for T > 1) are required");
+  if (((uintptr_t)a.actions & 15) != 0) return set_err(-1, "actions must be 16-byte aligned");
+  if (h->cfg.flags & F16_FLAG_NO_AUTORESET) return set_err(-1, "rollout_random needs auto-reset");
+  a.s = h->soa; a.tmpl = h->tmpl; a.nonfinite = h->nonfinite;
+  a.E = env_args(h);
+  a.C = h->C;
+  a.icc.c = nullptr; a.icc.n = a.E.n;
+  if (h->mode) {  // cfg5 modes: every lane's next reset cached before the launch (its first reset in it)
+    if (int e = icc_prepare(h, st, true)) return e;
+    a.icc = h->icc;
+    h->icc_steps = 0;  // the rollout consumed rows: the next windowed step refills
+  }
+  // two waves per SIMD when there are more waves than SIMDs (the 256-register build)
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0) cus = 256;
+  int occ = ((int64_t)a.E.n + 63) / 64 > 4 * (int64_t)cus ? 2 : 1;
+  if (getenv("F16ENV_ROLL_OCC")) occ = atoi(getenv("F16ENV_ROLL_OCC")) == 2 ? 2 : 1;
+  using RollKernel = void (*)(RollArgs);
+  static const RollKernel table[2][4] = {
+      {f16_rollout_kernel<0, 1>, f16_rollout_kernel<1, 1>, f16_rollout_kernel<2, 1>, f16_rollout_kernel<3, 1>},
+      {f16_rollout_kernel<0, 2>, f16_rollout_kernel<1, 2>, f16_rollout_kernel<2, 2>, f16_rollout_kernel<3, 2>}};
+  hipLaunchKernelGGL(table[occ == 2 ? 1 : 0][h->mode & 3], dim3(nblocks(a.E.n)), dim3(BLOCK), 0, st, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T, const float* obs_prev,
                           float* obs, float* frames, float* actions, float* rewards, float* next_start,
                           float* last_start) {
   if (!h) return set_err(-1, "null handle");
-  if (T < 1) return set_err(-1, "T must be >= 1");
-  if (!obs_prev || !obs || !frames || !actions || !rewards || !last_start || (T > 1 && !next_start))
-    return set_err(-1, "obs_prev/obs/frames/actions/rewards/last_start (and next_start for T > 1) are required");
-  if (((uintptr_t)actions & 15) != 0) return set_err(-1, "actions must be 16-byte aligned");
-  if (h->mode != 0 || (h->cfg.flags & F16_FLAG_NO_AUTORESET))
-    return set_err(-1, "rollout_random needs the reference task (no cfg5 modes) with auto-reset");
-  if (h->cfg.stack_k > 8) return set_err(-1, "rollout_random keeps the stack in LDS: stack_k <= 8");
+  if (!obs_prev || !obs) return set_err(-1, "obs_prev/obs are required");
+  const int K = h->cfg.stack_k;
   RollArgs a;
-  a.s = h->soa; a.tmpl = h->tmpl; a.obs_prev = obs_prev; a.obs = obs; a.frames = frames; a.actions = actions;
-  a.rewards = rewards; a.next_start = next_start; a.last_start = last_start; a.nonfinite = h->nonfinite;
+  memset(&a, 0, sizeof a);
+  a.obs_prev = obs_prev; a.in_row = (int64_t)K * F16_OBS_DIM; a.in_pitch = F16_OBS_DIM;
+  a.out0 = obs; a.out1 = nullptr; a.out_row = (int64_t)K * F16_OBS_DIM; a.out_pitch = F16_OBS_DIM;
+  a.out_slot = F16_OBS_DIM;
+  a.frames = frames; a.actions = actions; a.rewards = rewards; a.next_start = next_start; a.last_start = last_start;
   a.seed = seed; a.step0 = step0; a.T = T;
-  a.E = env_args(h);
-  a.C = h->C;
-  const size_t ring = sizeof(float) * h->cfg.stack_k * BLOCK * RING_PITCH;
-  hipLaunchKernelGGL(f16_rollout_kernel, dim3(nblocks(a.E.n)), dim3(BLOCK), ring, (hipStream_t)stream, a);
+  a.clear_fresh = 0;
+  return rollout_launch(h, (hipStream_t)stream, a);
+}
+
+int f16env_window_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T, int32_t parity,
+                                 int32_t pos, int32_t pos_out, float* frames, float* actions, float* rewards,
+                                 float* next_start, float* last_start) {
+  if (!h) return set_err(-1, "null handle");
+  if (!h->wb.hist[0]) return set_err(-1, "f16env_window_bind first");
+  const int K = h->cfg.stack_k;
+  const int64_t Th = h->wb.T;
+  if (pos < K - 1 || pos >= Th || pos_out < K - 1 || pos_out >= Th)
+    return set_err(-1, "window positions must be in [K-1, T-1]");
+  if (pos_out - K + 1 <= pos && pos - K + 1 <= pos_out)
+    return set_err(-1, "the output window must not overlap the input window");
+  int64_t P, Q;
+  window_strides(h, Th, P, Q);
+  const int b = parity & 1;
+  RollArgs a;
+  memset(&a, 0, sizeof a);
+  a.obs_prev = h->wb.hist[b] + (int64_t)(pos - K + 1) * P; a.in_row = Q; a.in_pitch = P;
+  a.out0 = h->wb.hist[0] + (int64_t)(pos_out - K + 1) * P;
+  a.out1 = h->wb.hist[1] + (int64_t)(pos_out - K + 1) * P;
+  a.out_row = Q; a.out_pitch = P; a.out_slot = WPITCH;
+  a.frames = frames; a.actions = actions; a.rewards = rewards; a.next_start = next_start; a.last_start = last_start;
+  a.seed = seed; a.step0 = step0; a.T = T;
+  a.clear_fresh = 1;  // both histories hold the whole final window
+  return rollout_launch(h, (hipStream_t)stream, a);
+}
+
+// on_policy_algorithm.py:236-245 over a device batch: rewards[i] += gamma * terminal_values[i]
+// where the lane's episode ended by truncation only (TimeLimit.truncated), float32 per-op
+// rounding as SB3 (gamma rounded to float32, the product, then the sum; no FMA)
+__global__ void f16_bootstrap_kernel(int64_t n, float* __restrict__ rew, const uint8_t* __restrict__ term,
+                                     const uint8_t* __restrict__ trunc, const float* __restrict__ tv, float g) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (trunc[i] && !term[i]) rew[i] = rew[i] + g * tv[i];
+}
+
+int f16env_bootstrap_timeouts(void* stream, int64_t n, float* rewards, const uint8_t* terminated,
+                              const uint8_t* truncated, const float* terminal_values, double gamma) {
+  if (n < 0) return set_err(-1, "n must be >= 0");
+  if (n == 0) return 0;
+  if (!rewards || !terminated || !truncated || !terminal_values) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_bootstrap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                     rewards, terminated, truncated, terminal_values, (float)gamma);
   HIPCHK(hipGetLastError());
   return 0;
 }
+
+int f16env_abi_version(void) { return F16ENV_ABI_VERSION; }
 
 int f16env_get_state(f16env_t h, void* stream, double* canon) {
   if (!h || !canon) return set_err(-1, "null argument");
@@ -2351,6 +2664,7 @@ int f16env_get_state(f16env_t h, void* stream, double* canon) {
 int f16env_set_state(f16env_t h, void* stream, const double* canon) {
   if (!h || !canon) return set_err(-1, "null argument");
   hipStream_t st = (hipStream_t)stream;
+  h->icc_steps = 0;  // episode counters may change: the next windowed step refills the reset cache
   int* wind_any = reinterpret_cast<int*>(h->nonfinite + 1);
   HIPCHK(hipMemsetAsync(wind_any, 0, sizeof(int), st));
   hipLaunchKernelGGL(f16_set_state_kernel, dim3(nblocks(h->soa.n)), dim3(BLOCK), 0, st, h->soa, canon, h->C, wind_any);
@@ -2393,8 +2707,18 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
   if (!rewards || !values || !episode_starts || !last_values || !dones || !advantages || !returns)
     return set_err(-1, "null argument");
   const float g = (float)gamma, gl = (float)(gamma * gae_lambda);
-  hipLaunchKernelGGL(f16_gae_kernel, dim3((unsigned)((n_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     n_steps, n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
+  // half-populated waves while that still leaves >= one wave per SIMD's worth of envs idle
+  // otherwise (cfg4: 32 768 envs -> 1 024 waves); F16ENV_GAE_LPW=64|32 overrides
+  static const int lpw_env = getenv("F16ENV_GAE_LPW") ? atoi(getenv("F16ENV_GAE_LPW")) : 0;
+  const int lpw = lpw_env == 64 || lpw_env == 32 ? lpw_env : (n_envs <= 1024 * 32 ? 32 : 64);
+  const int64_t blocks = (n_envs + lpw - 1) / lpw;
+  if (blocks > 0x7fffffffLL) return set_err(-1, "n_envs too large");
+  if (lpw == 32)
+    hipLaunchKernelGGL((f16_gae_kernel<16, 32>), dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, n_steps,
+                       n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
+  else
+    hipLaunchKernelGGL((f16_gae_kernel<16, 64>), dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, n_steps,
+                       n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
   HIPCHK(hipGetLastError());
   return 0;
 }

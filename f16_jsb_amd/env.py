@@ -22,7 +22,7 @@ import numpy as np
 from . import spaces
 from ._lib import F16EnvError, check, lib
 from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
-                  F16_FLAG_OBS_CHECK,
+                  F16_FLAG_OBS_CHECK, F16_SLOT_CLIP,
                   F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
@@ -299,30 +299,42 @@ class F16Envs:
                 raise ValueError("done_idx and n_done go together")
             self._need(done_idx, (self.n,), t.int32, "done_idx")
             self._need(n_done, (1,), t.int32, "n_done")
+        s, cur, p = self._advance()
+        if done_idx is None:  # the common case: five arguments, the rest bound at creation
+            check(self._step_bound(self._h, s, act.data_ptr(), cur, p), "f16env_window_step_bound")
+        else:
+            check(self._step_win_fn(self._h, s, act.data_ptr(), self._hist_ptr[cur], self._hist_ptr[cur ^ 1], self.T,
+                                    p, *self._win_ptr, _ptr(done_idx), _ptr(n_done)), "f16env_step_window")
+        return self._advanced(cur, p)
+
+    def _advance(self):
+        """(stream, parity, position) of the next windowed step: the new frame goes to position
+        p+1 of both histories (after a restart when p+1 reaches T)."""
         s = self._stream_int()
         p = self._p + 1
         if p >= self.T:  # move the last K-1 frames to the front of both histories
             check(lib().f16env_window_restart(self._h, s, self._hist_ptr[0], self._hist_ptr[1], self.T, self._p),
                   "f16env_window_restart")
             p = self.k - 1
-        cur = self._cur ^ 1
-        if done_idx is None:  # the common case: five arguments, the rest bound at creation
-            check(self._step_bound(self._h, s, act.data_ptr(), cur, p), "f16env_window_step_bound")
-        else:
-            check(self._step_win_fn(self._h, s, act.data_ptr(), self._hist_ptr[cur], self._hist_ptr[cur ^ 1], self.T,
-                                    p, *self._win_ptr, _ptr(done_idx), _ptr(n_done)), "f16env_step_window")
+        return s, self._cur ^ 1, p
+
+    def _advanced(self, cur, p) -> StepOut:
         self._cur, self._p = cur, p
         self.terminal_obs = self._window(1)
         return StepOut(self._window(), self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return,
                        self.ep_len)
 
     def step_rollout(self, seed: int, step: int, frame=None, actions=None, rewards=None, next_start=None,
-                     policy_actions=None, features=None) -> StepOut:
-        """One env step that also writes one rollout-buffer slot (f16env_step_rollout): the
-        newest frame of the observation acted on, the actions, the rewards and the next slot's
-        episode starts, with no extra launch. policy_actions None: actions drawn in-kernel
-        from the sample_actions(seed, step) stream (bit-identical)."""
-        self._no_window("step_rollout")
+                     policy_actions=None, features=None, next_frame=None, clip: bool = False) -> StepOut:
+        """One env step that also writes one rollout-buffer slot, with no extra launch
+        (f16env_step_rollout / f16env_window_step_rollout): the actions, the rewards and the next
+        slot's episode starts, and one frame of the frame-deduplicated log -- the contiguous
+        layout writes `frame` (the newest frame of the observation acted on), the windowed layout
+        `next_frame` (the newest frame of the returned observation, i.e. the next slot's frame).
+        policy_actions None: actions drawn in-kernel from the sample_actions(seed, step) stream
+        (bit-identical). clip: the env steps np.clip(policy_actions, low, high) over the action
+        Box (on_policy_algorithm.py:216) while `actions` receives policy_actions unclipped
+        (:247-254)."""
         t = self.torch
         act = None
         if policy_actions is not None:
@@ -335,7 +347,12 @@ class F16Envs:
                 act = self._act
             if tuple(act.shape) != (self.n, 4):
                 raise ValueError("policy_actions must be (N, 4), got %s" % (tuple(act.shape),))
+        if self.window and frame is not None:
+            raise ValueError("the windowed layout writes next_frame (the returned observation's newest frame), not frame")
+        if not self.window and next_frame is not None:
+            raise ValueError("the contiguous layout writes frame (the acted-on observation's newest frame), not next_frame")
         self._need(frame, (self.n, F16_OBS_DIM), t.float32, "frame")
+        self._need(next_frame, (self.n, F16_OBS_DIM), t.float32, "next_frame")
         self._need(actions, (self.n, 4), t.float32, "actions")
         self._need(rewards, (self.n,), t.float32, "rewards")
         self._need(next_start, (self.n,), t.float32, "next_start")
@@ -343,7 +360,13 @@ class F16Envs:
                                      or not features.is_contiguous()):
             raise ValueError("features must be a contiguous float32 (N, K, 17) tensor")
         slot = RolloutSlot(int(seed) & 0xFFFFFFFFFFFFFFFF, int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(frame),
-                           _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(features))
+                           _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(features), _ptr(next_frame),
+                           F16_SLOT_CLIP if clip else 0, 0)
+        if self.window:
+            s, cur, p = self._advance()
+            check(lib().f16env_window_step_rollout(self._h, s, ctypes.byref(slot), _ptr(act), cur, p),
+                  "f16env_window_step_rollout")
+            return self._advanced(cur, p)
         prev = self._obs[self._cur]
         nxt = self._obs[self._cur ^ 1]
         check(lib().f16env_step_rollout(self._h, self._stream(), ctypes.byref(slot), _ptr(act), _ptr(prev), _ptr(nxt),
@@ -354,25 +377,40 @@ class F16Envs:
 
     def rollout_random(self, seed: int, step0: int, n_steps: int, frames, actions, rewards, next_start,
                        last_start) -> None:
-        """n_steps env steps in ONE launch under the uniform random policy (f16env_rollout_random:
-        actions from the sample_actions(seed, step0 + t) stream, state kept on-chip): writes the
-        rollout slots frames (T, N, 15), actions (T, N, 4), rewards (T, N), next_start (T-1, N)
+        """n_steps env steps in ONE launch under the uniform random policy (f16env_rollout_random /
+        f16env_window_rollout_random: actions from the sample_actions(seed, step0 + t) stream,
+        state kept on-chip): writes the rollout slots frames (T, N, 15) (frames[t] = newest frame
+        of the observation step t acts on), actions (T, N, 4), rewards (T, N), next_start (T-1, N)
         (episode starts of slots 1..T-1) and last_start (N,), and leaves the env at its
-        observation after the last step (self.obs). The same actions and episode starts as n_steps
-        step_rollout calls; frames and rewards equal up to fp32 rounding."""
-        self._no_window("rollout_random")
+        observation after the last step (self.obs). Bit-identical to n_steps step_rollout calls.
+        Any stack_k and mode (cfg5: random ICs + gusts). Windowed layout: the final observation
+        is written into both histories at a window beside the current one; no terminal
+        observation is kept for the last step's finished lanes."""
         T = int(n_steps)
         n = self.n
         for name, x, shape in (("frames", frames, (T, n, F16_OBS_DIM)), ("actions", actions, (T, n, 4)),
                                ("rewards", rewards, (T, n)), ("last_start", last_start, (n,))):
-            if tuple(x.shape) != shape or x.dtype != self.torch.float32 or not x.is_contiguous():
-                raise ValueError("%s must be a contiguous float32 %s tensor" % (name, shape))
-        if T > 1 and (next_start is None or tuple(next_start.shape) != (T - 1, n) or not next_start.is_contiguous()):
+            if tuple(x.shape) != shape or x.dtype != self.torch.float32 or not x.is_contiguous() \
+                    or x.device != self.device:
+                raise ValueError("%s must be a contiguous float32 %s tensor on %s" % (name, shape, self.device))
+        if T > 1 and (next_start is None or tuple(next_start.shape) != (T - 1, n) or not next_start.is_contiguous()
+                      or next_start.dtype != self.torch.float32 or next_start.device != self.device):
             raise ValueError("next_start must be a contiguous float32 (T-1, N) tensor")
+        sd, st = int(seed) & 0xFFFFFFFFFFFFFFFF, int(step0) & 0xFFFFFFFFFFFFFFFF
+        if self.window:
+            k, p = self.k, self._p
+            q = p + k if p + k < self.T else k - 1  # the output window: beside the input one
+            if q - k + 1 <= p and p - k + 1 <= q:
+                raise F16EnvError("history too short for the rollout's output window (T = %d, K = %d)" % (self.T, k))
+            check(lib().f16env_window_rollout_random(self._h, self._stream(), sd, st, T, self._cur, p, q, _ptr(frames),
+                                                     _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(last_start)),
+                  "f16env_window_rollout_random")
+            self._p = q
+            self.terminal_obs = self._window(1)
+            return
         prev = self._obs[self._cur]
         nxt = self._obs[self._cur ^ 1]
-        check(lib().f16env_rollout_random(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                                          int(step0) & 0xFFFFFFFFFFFFFFFF, T, _ptr(prev), _ptr(nxt), _ptr(frames),
+        check(lib().f16env_rollout_random(self._h, self._stream(), sd, st, T, _ptr(prev), _ptr(nxt), _ptr(frames),
                                           _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(last_start)),
               "f16env_rollout_random")
         self._cur ^= 1

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 
 import torch
 
-from .abi import F16_FLAG_GUSTS, F16_FLAG_NO_AUTORESET, F16_FLAG_RANDOM_IC, F16_OBS_DIM
+from .abi import F16_FLAG_NO_AUTORESET, F16_OBS_DIM
 
 FIELDS = ("frames", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns")
 
@@ -90,81 +90,122 @@ class DeviceRolloutBuffer:
         return {f: getattr(self, f) for f in FIELDS} | {"obs0": self.obs0}
 
 
-def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int, step0: int = 0, values_fn=None, fused: bool = True,
-                    persistent: bool = True):
-    """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors with random
-    policy actions from the device Philox stream (the policy network is out of scope; values
-    and log-probs are zeros unless ``values_fn(obs) -> (values, log_probs)`` is given).
-    Starts from envs' current observation; returns (last_values, last_dones) for GAE.
+ACTION_LOW = (-1.0, -1.0, -1.0, 0.0)   # jsbsim_gym.py:143-148 action Box
+ACTION_HIGH = (1.0, 1.0, 1.0, 1.0)
 
-    fused: each step is ONE launch (f16env_step_rollout) that draws the actions in-kernel and
-    writes the slot's frame / actions / rewards / next episode starts itself, instead of a
-    sampling launch, the step and six buffer copies (RolloutBuffer.add, buffers.py:440-479).
-    persistent (with no values_fn, the reference task and K <= 8): the whole rollout is ONE
-    launch (f16env_rollout_random) that keeps every env's state on-chip across the steps: the
-    same actions and episode starts, frames / rewards equal up to fp32 rounding."""
+
+def np_clip_actions(a):
+    """np.clip(actions, action_space.low, action_space.high) (on_policy_algorithm.py:216) in
+    torch with numpy's clip-ufunc semantics: min(max(x, lo), hi), max(a, b) = a if a is NaN or
+    a > b else b (so NaN passes and -0 clips to +0 at a 0 bound) -- the in-kernel clip
+    (f16env.hip np_clip) computes the same."""
+    lo = torch.tensor(ACTION_LOW, dtype=a.dtype, device=a.device)
+    hi = torch.tensor(ACTION_HIGH, dtype=a.dtype, device=a.device)
+    m = torch.where(torch.isnan(a) | (a > lo), a, lo)
+    return torch.where(torch.isnan(m) | (m < hi), m, hi)
+
+
+def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 0, policy_fn=None, value_fn=None,
+                    fused: bool = True, persistent: bool = True):
+    """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors. Starts from the
+    envs' current observation; returns (last_values, last_dones) for GAE (:258-262).
+
+    policy_fn(obs) -> (actions, values, log_probs): the policy in the loop (:199-202), called on
+    the (N, K, 15) device observation. The env steps np.clip(actions, low, high) (:216; clipped
+    in the step kernel), the buffer stores the UNCLIPPED actions with the values and log-probs
+    (:247-254); a lane that ended by truncation alone bootstraps rewards += gamma *
+    V(terminal_obs) (:236-245, f16env_bootstrap_timeouts: V is evaluated on the whole batch of
+    terminal observations, no host sync, only those lanes' rewards change); V = value_fn(obs) ->
+    values when given, else policy_fn's values; last_values = V(final obs).
+    policy_fn None: the uniform random policy from the device Philox stream (seed, step0 + t),
+    values and log-probs zero, no bootstrap.
+
+    fused: each step is ONE launch (f16env_step_rollout / f16env_window_step_rollout) that takes
+    (or draws) the actions and writes the slot's actions / rewards / next episode starts and one
+    frame of the frame-deduplicated log itself, instead of a sampling launch, the step and six
+    buffer copies (RolloutBuffer.add, buffers.py:440-479).
+    persistent (no policy_fn): the whole rollout is ONE launch (f16env_rollout_random /
+    f16env_window_rollout_random) that keeps every env's state on-chip across the steps:
+    bit-identical to the fused launches."""
+
     dev = buf.device
     n = buf.n_envs
+    T = buf.n_steps
     zeros = torch.zeros(n, dtype=torch.float32, device=dev)
     obs = envs.obs
     starts = getattr(envs, "_last_episode_starts", None)
     if starts is None:
         starts = torch.ones(n, dtype=torch.float32, device=dev)
     buf.reset()
-    use_fused = fused and hasattr(envs, "step_rollout") and buf.frames[0].data_ptr() % 16 == 0 \
-        and (n * F16_OBS_DIM * 4) % 16 == 0
-    use_persistent = (use_fused and persistent and values_fn is None and hasattr(envs, "rollout_random")
-                      and envs.k <= 8 and not (envs.cfg.flags & (F16_FLAG_NO_AUTORESET | F16_FLAG_RANDOM_IC | F16_FLAG_GUSTS))
-                      and buf.actions.data_ptr() % 16 == 0)
+    window = bool(getattr(envs, "window", False))
+    vfn = value_fn if value_fn is not None else (lambda o: policy_fn(o)[1])
+    use_fused = fused and hasattr(envs, "step_rollout") and buf.actions.data_ptr() % 16 == 0 \
+        and (window or (buf.frames[0].data_ptr() % 16 == 0 and (n * F16_OBS_DIM * 4) % 16 == 0))
+    use_persistent = use_fused and persistent and policy_fn is None and hasattr(envs, "rollout_random") \
+        and not (envs.cfg.flags & F16_FLAG_NO_AUTORESET)
+    last_v = zeros
     if use_persistent:
         carry = torch.empty(n, dtype=torch.float32, device=dev)
         buf.obs0.copy_(obs)
         buf.episode_starts[0].copy_(starts)
-        T = buf.n_steps
         envs.rollout_random(seed, step0, T, buf.frames, buf.actions, buf.rewards,
                             buf.episode_starts[1:] if T > 1 else None, carry)
         obs = envs.obs
         buf.pos = T
         starts = carry
     elif use_fused:
+        from ._lib import check, lib
         carry = torch.empty(n, dtype=torch.float32, device=dev)
         buf.obs0.copy_(obs)
         buf.episode_starts[0].copy_(starts)
-        T = buf.n_steps
+        if window:  # the log's first frame; step t then writes frames[t + 1] (the returned obs's newest)
+            buf.frames[0].copy_(obs[:, -1])
         for t in range(T):
-            if values_fn is not None:
-                v, lp = values_fn(obs)
+            act = None
+            if policy_fn is not None:
+                act, v, lp = policy_fn(obs)
                 buf.values[t].copy_(v.reshape(-1))
                 buf.log_probs[t].copy_(lp.reshape(-1))
             nxt = buf.episode_starts[t + 1] if t + 1 < T else carry
-            out = envs.step_rollout(seed, step0 + t, frame=buf.frames[t], actions=buf.actions[t],
-                                    rewards=buf.rewards[t], next_start=nxt)
-            if values_fn is not None:
-                tv, _ = values_fn(out.terminal_obs)
-                buf.rewards[t].copy_(bootstrap_timeouts(buf.rewards[t], out.terminated, out.truncated, tv, buf.gamma))
+            frame_kw = ({"next_frame": buf.frames[t + 1] if t + 1 < T else None} if window
+                        else {"frame": buf.frames[t]})
+            out = envs.step_rollout(seed, step0 + t, actions=buf.actions[t], rewards=buf.rewards[t], next_start=nxt,
+                                    policy_actions=act, clip=policy_fn is not None, **frame_kw)
+            if policy_fn is not None:  # timeout bootstrap on the step's terminal observations
+                tv = vfn(out.terminal_obs).reshape(-1).to(torch.float32).contiguous()
+                check(lib().f16env_bootstrap_timeouts(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n,
+                                                      buf.rewards[t].data_ptr(), out.terminated.data_ptr(),
+                                                      out.truncated.data_ptr(), tv.data_ptr(), buf.gamma),
+                      "f16env_bootstrap_timeouts")
             obs = out.obs
         buf.pos = T
         starts = carry
     else:
-        for t in range(buf.n_steps):
-            act = envs.sample_actions(seed, step0 + t)
-            v, lp = values_fn(obs) if values_fn is not None else (zeros, zeros)
-            out = envs.step(act)
+        for t in range(T):
+            obs = obs.clone()  # (an env may reuse its observation buffer in the step below)
+            if policy_fn is not None:
+                act, v, lp = policy_fn(obs)
+                act = act.reshape(n, -1).to(torch.float32)
+                out = envs.step(np_clip_actions(act).contiguous())
+            else:
+                act, v, lp = envs.sample_actions(seed, step0 + t), zeros, zeros
+                out = envs.step(act)
             rew = out.rew
-            if values_fn is not None:
-                tv, _ = values_fn(out.terminal_obs)
-                rew = bootstrap_timeouts(rew, out.terminated, out.truncated, tv, buf.gamma)
+            if policy_fn is not None:
+                rew = bootstrap_timeouts(rew, out.terminated, out.truncated, vfn(out.terminal_obs), buf.gamma)
             buf.add(obs, act, rew, starts, v, lp)
             obs = out.obs
             starts = (out.terminated | out.truncated).to(torch.float32)
     envs._last_episode_starts = starts
-    last_v = values_fn(obs)[0] if values_fn is not None else zeros
+    if policy_fn is not None:
+        last_v = vfn(obs).reshape(-1).to(torch.float32)
     return last_v, starts
 
 
 def bootstrap_timeouts(rewards, terminated, truncated, terminal_values, gamma: float):
     """on_policy_algorithm.py:236-245 vectorised: for lanes that ended by truncation only,
-    rewards += gamma * V(terminal_observation) (float32 per-op rounding as SB3)."""
+    rewards += gamma * V(terminal_observation) (float32 per-op rounding as SB3; the HIP kernel
+    f16env_bootstrap_timeouts computes the same in place)."""
     mask = truncated.bool() & ~terminated.bool()
     g = torch.tensor(gamma, dtype=torch.float32, device=rewards.device)
     add = g * terminal_values.reshape(-1).to(torch.float32)

@@ -22,6 +22,11 @@
  *   f16env_trim     <- no reference equivalent (the reference never trims; BASELINE cfg 2)
  *   f16env_sample_actions <- action_space.sample() (jsbsim_gym.py:575), device Philox
  *   f16env_step_rollout <- f16env_step + buffers.py:440-479 RolloutBuffer.add (8f rank 1)
+ *   f16env_window_step_rollout <- the same on windowed observations, with the policy's actions
+ *                      clipped to the Box in-kernel (on_policy_algorithm.py:199-218)
+ *   f16env_rollout_random / f16env_window_rollout_random <- on_policy_algorithm.py:194-262's
+ *                      loop under the uniform random policy, one launch
+ *   f16env_bootstrap_timeouts <- on_policy_algorithm.py:236-245 (timeout bootstrap)
  *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
  *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
  *   f16env_poses    <- jsbsim_gym.py:381-415 JSBSimEnv.render state -> Viewer poses (8f rank 4)
@@ -36,7 +41,11 @@
 extern "C" {
 #endif
 
-#define F16ENV_ABI_VERSION 2
+/* 3 (round 4): f16env_step_kernel_name takes the handle (was (void)); f16env_set_state keeps the
+ * windowed layout's FRESH mark; the rollout slot gained next_frame / flags (F16_SLOT_CLIP);
+ * f16env_rollout_random has no stack_k / mode limits; new f16env_window_step_rollout,
+ * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_abi_version. */
+#define F16ENV_ABI_VERSION 3
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
 #define F16_OBS_DIM 15
@@ -183,8 +192,9 @@ int f16env_destroy(f16env_t h);
  * can carry steady wind: config IC / random-IC box wind, or set by f16env_set_state). */
 int f16env_step_mode(f16env_t h);
 
-/* Bytes of device state held by the handle / persistent bytes per env (roofline S: 256 B,
- * +32 B for the wind kernels' steady-wind and gust columns). */
+/* Bytes of device state held by the handle (the SoA state, plus cfg5 modes' reset cache of
+ * 336 B per env) / persistent bytes per env a step moves (roofline S: 256 B, +32 B for the wind
+ * kernels' steady-wind and gust columns). */
 size_t f16env_state_bytes(f16env_t h);
 int f16env_state_bytes_per_env(void);
 
@@ -257,16 +267,25 @@ int f16env_step_window_nt(f16env_t h);
 
 /* One env step that also fills one slot of a device rollout buffer (SURVEY.md 8f rank 1,
  * replacing the per-step stable_baselines3 RolloutBuffer.add, buffers.py:440-479, and the
- * action sampling of collect_rollouts, on_policy_algorithm.py:194-218, with no extra launch).
- * Every pointer of the slot may be NULL (not written):
+ * action sampling / clipping of collect_rollouts, on_policy_algorithm.py:194-218, with no
+ * extra launch). Every pointer of the slot may be NULL (not written):
  *   frame      N x 15 float: newest frame of obs_prev, i.e. of the observation acted on
- *              (frame-deduplicated storage; f16_jsb_amd/rollout.py rebuilds stacks)
- *   actions    N x 4 float: the actions applied
+ *              (frame-deduplicated storage; f16_jsb_amd/rollout.py rebuilds stacks).
+ *              Contiguous layout only (f16env_step_rollout).
+ *   next_frame N x 15 float: newest frame of the RETURNED observation (the next slot's frame;
+ *              the reset frame where the lane finished). Windowed layout only
+ *              (f16env_window_step_rollout): written from the same LDS staging as the window.
+ *   actions    N x 4 float: the actions as given (SB3 stores the unclipped policy output,
+ *              on_policy_algorithm.py:247-254)
  *   rewards    N float: the step's rewards (same values as rew)
  *   next_start N float: 1.0 where the lane finished (episode_starts of the NEXT slot), else 0
  *   features   N x K x 17 float: policy features of the returned observation (below)
+ *   flags      F16_SLOT_CLIP: the env steps np.clip(act, low, high) over the action Box
+ *              (on_policy_algorithm.py:216; numpy's clip ufunc semantics, NaN passes), while
+ *              `actions` keeps act unclipped
  * act == NULL draws the actions in-kernel from the f16env_sample_actions stream
  * (act_seed, act_step), bit-identical to f16env_sample_actions followed by f16env_step. */
+#define F16_SLOT_CLIP 0x1
 typedef struct f16env_rollout_slot {
   uint64_t act_seed, act_step;
   float* frame;
@@ -276,28 +295,56 @@ typedef struct f16env_rollout_slot {
   float* features;  /* N x K x 17: policy features of the returned obs (features.py:37-67, as
                        f16env_features), by a second launch in the same call (an epilogue
                        fused into the step kernel measured slower: +9.5 vs +9 us) */
+  float* next_frame;
+  uint32_t flags;
+  uint32_t reserved;
 } f16env_rollout_slot;
 int f16env_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                         const float* obs_prev, float* obs, float* rew, uint8_t* terminated, uint8_t* truncated,
                         float* terminal_obs, double* ep_return, int32_t* ep_len, int32_t* done_idx,
                         int32_t* n_done);
 
+/* f16env_step_rollout on windowed observations, with the buffers bound by f16env_window_bind
+ * (parity / pos as f16env_window_step_bound). slot->frame must be NULL (the window layout
+ * writes next_frame); slot->features reads the returned window in place. */
+int f16env_window_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
+                               int32_t parity, int32_t pos);
+
 /* T env steps of every lane in ONE launch under the uniform random policy (the actions are the
  * f16env_sample_actions stream (seed; env id, step0 + t)): SURVEY.md 8f rank 1's rollout with
- * the policy network out of scope. The state stays in registers and the last K frames in LDS
- * for the whole rollout; per step only the rollout slot is written:
- *   frames     T x N x 15  newest frame of the observation acted on at step t
+ * the policy network out of scope. The state stays in registers for the whole rollout; per step
+ * only the rollout slot is written:
+ *   frames     T x N x 15  newest frame of the observation acted on at step t (frames[0]: of
+ *                          obs_prev; frames[t+1] is written by step t)
  *   actions    T x N x 4   rewards T x N
  *   next_start (T-1) x N   1.0 where the lane finished at step t (episode_starts of slot t+1)
  *   last_start N           the same for step T-1
- * obs_prev / obs: N x K x 15 before step 0 / after step T-1 (may alias). The same actions and
- * episode starts as T calls of f16env_step_rollout(seed, step0 + t, ...), frames and rewards
- * equal up to fp32 rounding (the same arithmetic compiled in another kernel). Reference task
- * only (no cfg5 modes, auto-reset on), stack_k <= 8. Replaces on_policy_algorithm.py:194-262's
- * loop for that policy. */
+ * obs_prev / obs: N x K x 15 before step 0 / after step T-1 (distinct buffers; the final stack
+ * is rebuilt from the frame log). The same actions and episode starts, frames and rewards as T
+ * calls of f16env_step_rollout(seed, step0 + t, ...) (bit-identical). Any stack_k, the cfg5
+ * modes included (a lane's first reset in the rollout comes from the reset cache, later ones
+ * run their RunIC in the kernel); auto-reset on. Replaces on_policy_algorithm.py:194-262's loop
+ * for that policy. */
 int f16env_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T,
                           const float* obs_prev, float* obs, float* frames, float* actions,
                           float* rewards, float* next_start, float* last_start);
+/* The same on the bound window histories: the observation before step 0 is hist[parity]'s
+ * window ending at pos, the final observation is written into BOTH histories' windows ending at
+ * pos_out (which must not overlap the input window), so the next windowed step continues from
+ * parity `parity`, position pos_out, with no lane needing a fresh-window fill. (No terminal
+ * observation is produced for the last step's finished lanes.) */
+int f16env_window_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T,
+                                 int32_t parity, int32_t pos, int32_t pos_out, float* frames, float* actions,
+                                 float* rewards, float* next_start, float* last_start);
+
+/* on_policy_algorithm.py:236-245 (timeout bootstrap, SB3 issue #633) over a device batch:
+ * rewards[i] += gamma * terminal_values[i] where truncated[i] && !terminated[i], float32 with
+ * SB3's rounding (f32(gamma) * v, then the sum). In place; stream-ordered; no handle needed. */
+int f16env_bootstrap_timeouts(void* stream, int64_t n, float* rewards, const uint8_t* terminated,
+                              const uint8_t* truncated, const float* terminal_values, double gamma);
+
+/* F16ENV_ABI_VERSION of the built library (a binding checks it against its header). */
+int f16env_abi_version(void);
 
 /* Lanes quarantined by F16_FLAG_NAN_GUARD since create (waits for `stream`). */
 int f16env_nonfinite_count(f16env_t h, void* stream, uint64_t* count);

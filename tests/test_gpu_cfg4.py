@@ -1,5 +1,6 @@
 """BASELINE cfg4's per-GPU share through the kernel that runs it: 32 768 envs x PPO n_steps
-2 048, K = 4, one f16_rollout_kernel launch (f16env_rollout_random; bench.py rollout_bench),
+2 048, K = 4, one f16_rollout_kernel launch (f16env_rollout_random / f16env_window_rollout_random
+in the windowed layout; bench.py rollout_bench),
 which replaces n_steps iterations of collect_rollouts' env.step + RolloutBuffer.add
 (on_policy_algorithm.py:194-262, buffers.py:440-479; the env step is jsbsim_gym.py:199-287).
 
@@ -31,11 +32,14 @@ from f16_jsb_amd.abi import F16C_EP_COUNT, F16C_STEP  # noqa: E402
 N, K, T, SEED = 32768, 4, 2048, 71
 
 
-def test_cfg4_rollout_kernel_per_gpu_share(gpu):
+@pytest.mark.parametrize("layout", ["window", "contiguous"])
+def test_cfg4_rollout_kernel_per_gpu_share(gpu, layout):
+    """window: f16env_window_rollout_random (the final observation written into both window
+    histories); contiguous: f16env_rollout_random -- the same kernel, f16_rollout_kernel<0, 1>."""
     import torch
     from f16_jsb_amd.env import F16Envs
     from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout, rebuild_observations
-    ref, g = OracleEnvs(N, stack_k=K, seed=SEED), F16Envs(N, stack_k=K, seed=SEED)
+    ref, g = OracleEnvs(N, stack_k=K, seed=SEED), F16Envs(N, stack_k=K, seed=SEED, obs_layout=layout)
     o = ref.reset()
     g.reset()
     s = ref.get_state()

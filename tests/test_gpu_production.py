@@ -185,6 +185,37 @@ def test_cfg5_production_instance_131072(torch_mod, layout, done_list):
     g.close()
 
 
+def test_cfg5_inline_runic_resets_131072(torch_mod):
+    """cfg5's windowed step resets a finished lane from the reset cache when it holds that
+    lane's next episode (f16_ic_fill_kernel, every 64 windowed steps), and a lane that finishes
+    again within the same refill period runs its RunIC inside the step (f16env.hip step_body
+    in_step_reset -> lane_reset_mode). With max_steps = 5 every lane truncates every 5 steps, so
+    after each lane's first (cached) reset every later reset of the 30 steps is an in-step RunIC:
+    the cfg5 bench's instance f16_step_win_nt_kernel<3, 2> at 131 072 envs against the oracle --
+    done flags, episode counters and Philox goals bit-exact, reset frames at TOL_STEP."""
+    torch = torch_mod
+    from f16_jsb_amd.abi import F16C_EP_COUNT
+    from f16_jsb_amd.env import F16Envs
+    n = 131072
+    ref = OracleEnvs(n, stack_k=4, seed=43, cfg5=True, max_steps=5)
+    g = F16Envs(n, stack_k=4, seed=43, cfg5=True, max_steps=5, obs_layout="window")
+    assert g.step_kernel_name == "f16_step_win_nt_kernel<3, 2>", g.step_kernel_name
+    o = ref.reset()
+    g.reset()
+    _stagger(ref, g, o, every=1, span=5)  # phases spread over the 5 steps; the next step refills the cache
+    ep0 = ref.get_state()[:, F16C_EP_COUNT]
+    fin = _run_parity(torch, ref, g, 30, 37, TOL_RAND30 * 2, gust=True, tol_max=TOL_RAND30 * 10,
+                      early=(10, TOL_RAND30), done_list=False)
+    ep_r = ref.get_state()[:, F16C_EP_COUNT]
+    ep_g = g.get_state().cpu().numpy()[:, F16C_EP_COUNT]
+    np.testing.assert_array_equal(ep_g, ep_r)
+    resets = (ep_r - ep0).astype(np.int64)
+    inline = int(np.maximum(resets - 1, 0).sum())  # all but each lane's first reset of the 30 steps
+    assert fin == int(resets.sum()) and inline >= 4 * n, (fin, inline)
+    ref.close()
+    g.close()
+
+
 def test_reference_stack_k10_global_table_instance(torch_mod):
     """The reference's default stack K = 10 (jsbsim_gym.py:58) needs the whole LDS for the stack
     image, so the handle picks f16_step_gt_kernel<0> (tables from L1/L2): 4 096 envs, 30

@@ -119,3 +119,80 @@ def test_gather_to_rank0_gloo(world, chunk):
             np.testing.assert_array_equal(env_major(torch.as_tensor(v)).numpy(),
                                           np.concatenate([got["local%d" % r][f] for r in range(world)], axis=1))
     assert out["frames"].shape == (world, T, N, 15) and out["obs0"].shape == (world, N, K, 15)
+
+
+def test_np_clip_actions_matches_numpy():
+    """The clip SB3 applies before env.step (on_policy_algorithm.py:216), numpy's semantics
+    including NaN and signed zero (the kernel's np_clip computes the same)."""
+    from f16_jsb_amd.rollout import ACTION_HIGH, ACTION_LOW, np_clip_actions
+    rng = np.random.default_rng(3)
+    a = (rng.normal(size=(257, 4)) * 2).astype(np.float32)
+    a[:4] = [[np.nan, -0.0, np.inf, -0.0], [-np.inf, 0.0, -1.0, 1.0], [1.0, -1.0, -0.0, 0.0], [2.0, -2.0, 0.5, -3.0]]
+    want = np.clip(a, np.array(ACTION_LOW, np.float32), np.array(ACTION_HIGH, np.float32))
+    got = np_clip_actions(torch.as_tensor(a)).numpy()
+    np.testing.assert_array_equal(got, want)
+    assert np.array_equal(np.signbit(got), np.signbit(want))
+
+
+def _linear_policy(scale=3.0):
+    """A deterministic stand-in for SB3's policy(obs) -> (actions, values, log_probs) whose actions
+    leave the Box (so the clip matters) and whose value depends on the observation."""
+    g = torch.Generator().manual_seed(5)
+    W = torch.randn(15, 4, generator=g)
+    calls = []
+
+    def policy(obs):
+        x = obs[:, -1, :].to(torch.float32)
+        a = scale * torch.tanh(x @ W * 0.1) + torch.tensor([0.0, 0.0, 0.0, -0.5])
+        v = x[:, 1] * 0.25 - x[:, 0]
+        lp = -(a * a).sum(-1)
+        calls.append((obs.clone(), a.clone(), v.clone(), lp.clone()))
+        return a, v, lp
+
+    return policy, calls
+
+
+def test_collect_rollout_policy_in_the_loop_cpu():
+    """collect_rollouts (on_policy_algorithm.py:199-262) with a policy, host path over the CPU
+    stand-in env: the env steps the clipped actions, the buffer keeps the unclipped ones with the
+    values and log-probs, truncated-only lanes bootstrap gamma * V(terminal_obs), the last values
+    are V(final obs) -- against a direct restatement of SB3's loop on a second env."""
+    from fake_envs import FakeEnvs
+    from f16_jsb_amd.rollout import ACTION_HIGH, ACTION_LOW, collect_rollout
+    n, k, T, gamma = 6, 3, 11, 0.9
+    env = FakeEnvs(n, k=k, max_steps=4)
+    env.reset()
+    policy, calls = _linear_policy()
+    buf = DeviceRolloutBuffer(T, n, k, "cpu", gamma=gamma)
+    last_v, last_d = collect_rollout(env, buf, policy_fn=policy)
+    # SB3's loop, restated on numpy (float32), on an identical env
+    ref = FakeEnvs(n, k=k, max_steps=4)
+    obs = ref.reset().clone()
+    starts = np.ones(n, np.float32)
+    low, high = np.array(ACTION_LOW, np.float32), np.array(ACTION_HIGH, np.float32)
+    boot = 0
+    for t in range(T):
+        a, v, lp = policy(obs)
+        a, v, lp = a.numpy(), v.numpy(), lp.numpy()
+        out = ref.step(torch.as_tensor(np.clip(a, low, high)))
+        rewards = out.rew.numpy().copy()
+        term, trunc = out.terminated.numpy().astype(bool), out.truncated.numpy().astype(bool)
+        for idx in range(n):
+            if (term[idx] or trunc[idx]) and trunc[idx] and not term[idx]:
+                tv = policy(out.terminal_obs[idx][None].clone())[1].numpy()[0]
+                rewards[idx] = np.float32(rewards[idx] + np.float32(np.float32(gamma) * tv))
+                boot += 1
+        np.testing.assert_array_equal(buf.actions[t].numpy(), a, err_msg="unclipped actions @%d" % t)
+        np.testing.assert_array_equal(buf.values[t].numpy(), v)
+        np.testing.assert_array_equal(buf.log_probs[t].numpy(), lp)
+        np.testing.assert_array_equal(buf.rewards[t].numpy(), rewards, err_msg="bootstrapped rewards @%d" % t)
+        np.testing.assert_array_equal(buf.episode_starts[t].numpy(), starts)
+        np.testing.assert_array_equal(buf.frames[t].numpy(), obs[:, -1].numpy())
+        starts = (term | trunc).astype(np.float32)
+        obs = out.obs.clone()
+    assert boot > 0, "expected truncations inside the rollout"
+    np.testing.assert_array_equal(last_d.numpy(), starts)
+    np.testing.assert_array_equal(last_v.numpy(), policy(obs)[1].numpy())
+    # the env saw the clipped actions: FakeEnvs records a lane's action in its frame [3:7]
+    np.testing.assert_array_equal(env.obs.numpy(), obs.numpy())
+    assert np.abs(np.concatenate([c[1].numpy() for c in calls])).max() > 1.0  # the clip mattered
