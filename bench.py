@@ -278,6 +278,12 @@ def rollout_bench(args, dev, rank, world):
         envs.step(acts[t % 8])
     sync()
     plain_ms = (time.perf_counter() - tp0) / 512 * 1e3
+    # the two kernels alone (dispatch events of each launch): the rollout-slot build vs the plain
+    # windowed step, 256 launches each
+    small = DeviceRolloutBuffer(256, n, args.stack, dev)
+    roll_kern_ms, _, _ = envs.profile_kernel(lambda: collect_rollout(envs, small, args.seed + 5600, persistent=False), 256)
+    step_kern_ms, _, _ = envs.profile_kernel(lambda: [envs.step(acts[t % 8]) for t in range(256)], 256)
+    del small
     barrier()
     t0 = time.perf_counter()
     last_v, last_d = collect_rollout(envs, buf, args.seed + 4000)  # one persistent launch
@@ -372,6 +378,9 @@ def rollout_bench(args, dev, rank, world):
         "rollout_fused_ms_per_step": round(fused_ms, 5),
         "window_step_ms_same_envs": round(plain_ms, 5),
         "fused_over_plain_step": round(fused_ms / plain_ms, 4),
+        "rollout_step_kernel_ms": round(roll_kern_ms, 5),
+        "window_step_kernel_ms_same_envs": round(step_kern_ms, 5),
+        "rollout_step_kernel": envs.step_kernel_name.replace("false>", "true>") + " (the rollout-slot build)",
         **cont,
         "gae_ms": round(float(tt[1]) * 1e3, 3),
         "gae_kernel_ms": round(float(tt[4]), 4),

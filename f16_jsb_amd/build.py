@@ -16,6 +16,10 @@ OUT = os.path.join(HERE, "libf16env.so")
 # debug build: the same kernels with the F16_CHECK index / range invariants
 # compiled in (f16_device.h), read back by f16env_debug_checks; tests load it by F16ENV_LIB
 OUT_DEBUG = os.path.join(HERE, "libf16env_debug.so")
+# miscompile guard (test only): the same source at -O1 -- other instruction selection, scheduling
+# and register allocation, the same rounding (-ffp-contract=on fixes contraction per source
+# expression) -- compared bit for bit against the product by tests/test_gpu_o1_differential.py
+OUT_O1 = os.path.join(HERE, "libf16env_o1.so")
 DEPS = [SRC, os.path.join(HERE, "csrc", "f16_device.h"), os.path.join(HERE, "csrc", "f16_tables.h"),
         os.path.join(ROOT, "include", "f16env.h")]
 
@@ -27,10 +31,12 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = False) -> str:
-    out = OUT_DEBUG if debug else OUT
+def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = False, o1: bool = False) -> str:
+    out = OUT_DEBUG if debug else (OUT_O1 if o1 else OUT)
     if debug:
         extra = tuple(extra) + ("-DF16_DEBUG_CHECKS",)
+    if o1:
+        extra = tuple(extra) + ("-O1",)  # after the -O3 below: the last -O wins
     if not force and os.path.exists(out):
         t_out = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= t_out for d in DEPS):
@@ -57,4 +63,5 @@ def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = Fa
 
 
 if __name__ == "__main__":
-    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv, debug="--debug" in sys.argv))
+    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv, debug="--debug" in sys.argv,
+                o1="--o1" in sys.argv))

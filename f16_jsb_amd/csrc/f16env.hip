@@ -2767,7 +2767,8 @@ const char* f16env_step_kernel_name(f16env_t h) {
   static thread_local char buf[64];
   if (!h) return "";
   if (h->wb.hist[0]) {
-    snprintf(buf, sizeof buf, "f16_step_win%s_kernel<%d, %d>", h->win_nt ? "_nt" : "", h->mode & 3, h->win_occ);
+    // (as rocprofv3 demangles it: the plain step, not the rollout-slot build <.., true>)
+    snprintf(buf, sizeof buf, "f16_step_win%s_kernel<%d, %d, false>", h->win_nt ? "_nt" : "", h->mode & 3, h->win_occ);
   } else if (h->gt) {
     snprintf(buf, sizeof buf, "f16_step_gt_kernel<%d, false>", h->mode & 3);  // as rocprofv3 demangles it
   } else if ((h->mode & 3) == 0 && h->occ == 1) {

@@ -165,10 +165,6 @@ class F16Envs:
             return self._hist[b, :, p - self.k + 1:p + 1, :F16_OBS_DIM]
         return self._hist[b, p - self.k + 1:p + 1, :, :F16_OBS_DIM].transpose(0, 1)
 
-    def _no_window(self, what: str):
-        if self.window:
-            raise F16EnvError("%s is not available with obs_layout='window' (use obs_layout='contiguous')" % what)
-
     @property
     def obs(self):
         return self._window() if self.window else self._obs[self._cur]
@@ -375,6 +371,22 @@ class F16Envs:
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
+    def _step_rollout_raw(self, slot, act_ptr) -> StepOut:
+        """step_rollout with a prepared RolloutSlot and action address and no argument checks:
+        collect_rollout validates its buffers once per rollout and moves the slot's row
+        addresses itself (the per-step host cost is then the launch, not the checks)."""
+        if self.window:
+            s, cur, p = self._advance()
+            check(lib().f16env_window_step_rollout(self._h, s, ctypes.byref(slot), act_ptr, cur, p),
+                  "f16env_window_step_rollout")
+            return self._advanced(cur, p)
+        cur = self._cur
+        nxt = self._obs[cur ^ 1]
+        check(lib().f16env_step_rollout(self._h, self._stream_int(), ctypes.byref(slot), act_ptr, self._obs_ptr[cur],
+                                        self._obs_ptr[cur ^ 1], *self._out_ptr, None, None), "f16env_step_rollout")
+        self._cur = cur ^ 1
+        return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
+
     def rollout_random(self, seed: int, step0: int, n_steps: int, frames, actions, rewards, next_start,
                        last_start) -> None:
         """n_steps env steps in ONE launch under the uniform random policy (f16env_rollout_random /
@@ -390,7 +402,7 @@ class F16Envs:
         n = self.n
         for name, x, shape in (("frames", frames, (T, n, F16_OBS_DIM)), ("actions", actions, (T, n, 4)),
                                ("rewards", rewards, (T, n)), ("last_start", last_start, (n,))):
-            if tuple(x.shape) != shape or x.dtype != self.torch.float32 or not x.is_contiguous() \
+            if x is None or tuple(x.shape) != shape or x.dtype != self.torch.float32 or not x.is_contiguous() \
                     or x.device != self.device:
                 raise ValueError("%s must be a contiguous float32 %s tensor on %s" % (name, shape, self.device))
         if T > 1 and (next_start is None or tuple(next_start.shape) != (T - 1, n) or not next_start.is_contiguous()
@@ -887,12 +899,18 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
     are filled for the finished lanes (gymnasium's vector-info convention: a value array plus a
     "_key" boolean mask). ``reset(seed=s)`` seeds env i with s + i (the reference's
     default_rng(seed) goal, jsbsim_gym.py:312-323). Single-env semantics are jsbsim_gym.py's
-    JSBSimEnv wrapped in TimeLimit(1200) and PositionReward(1e-2) (jsbsim_gym.py:537-545)."""
+    JSBSimEnv wrapped in TimeLimit(1200) and PositionReward(1e-2) (jsbsim_gym.py:537-545).
+
+    Numpy mode returns observations as strided views of a pinned host mirror of the windowed
+    handle's frame histories (_HostWindow): an obs array stays valid until the step after next
+    (the next step leaves it intact, the one after overwrites it). A consumer that keeps
+    observations longer passes ``copy_obs=True`` (contiguous copies; whole-observation
+    device-to-host copies per step). ``infos["final_obs"]`` is always a copy."""
 
     metadata = {"autoreset_mode": "SameStep", "render_modes": []}
 
     def __init__(self, num_envs: int = 1, stack_k: int = 10, device=None, seed: int = 0,
-                 return_numpy: bool = True, envs=None, **kw):
+                 return_numpy: bool = True, envs=None, copy_obs: bool = False, **kw):
         if envs is None:  # as F16VecEnv: the windowed layout when observations go to the host
             kw.setdefault("obs_layout", "window" if return_numpy else "contiguous")
             envs = F16Envs(num_envs, stack_k=stack_k, device=device, seed=seed, **kw)
@@ -906,7 +924,8 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
         self.spec = None
         self.closed = False
         self.return_numpy = bool(return_numpy)
-        self._host = _staging(self.envs) if self.return_numpy else None
+        self.copy_obs = bool(copy_obs)
+        self._host = _staging(self.envs, self.copy_obs) if self.return_numpy else None
         self._t_start = time.time()
 
     def reset(self, *, seed=None, options=None):
@@ -923,7 +942,8 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
         self._t_start = time.time()
         if not self.return_numpy:
             return obs, {}
-        return self._host.fetch(obs, with_flags=False)[0], {}
+        o = self._host.fetch(obs, with_flags=False)[0]
+        return (np.array(o) if self.copy_obs else o), {}
 
     def step(self, actions):
         if not self.return_numpy:
@@ -958,6 +978,8 @@ class F16GymVectorEnv(*_bases(GymVectorEnv)):
             infos["_final_obs"] = done
             infos["episode"] = {"r": r, "l": ln, "t": np.where(done, t, 0.0)}
             infos["_episode"] = done
+        if self.copy_obs:
+            obs = np.array(obs)
         return obs, rew.copy(), term, trunc, infos
 
     def close(self, **kwargs):

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 
 import torch
 
-from .abi import F16_FLAG_NO_AUTORESET, F16_OBS_DIM
+from .abi import F16_FLAG_NO_AUTORESET, F16_OBS_DIM, F16_SLOT_CLIP, RolloutSlot
 
 FIELDS = ("frames", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns")
 
@@ -160,22 +160,50 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
         buf.episode_starts[0].copy_(starts)
         if window:  # the log's first frame; step t then writes frames[t + 1] (the returned obs's newest)
             buf.frames[0].copy_(obs[:, -1])
+        # the slot is built once and its row addresses moved per step (the buffer was allocated
+        # with these shapes on this device: no per-step checks on the launch path)
+        if getattr(envs, "device", dev) != dev:
+            raise ValueError("rollout buffer on %s, envs on %s" % (dev, envs.device))
+        raw = hasattr(envs, "_step_rollout_raw")
+        slot = RolloutSlot(int(seed) & 0xFFFFFFFFFFFFFFFF, 0, None, None, None, None, None, None,
+                           F16_SLOT_CLIP if policy_fn is not None else 0, 0)
+        fr0, ac0, rw0, st0 = (buf.frames.data_ptr(), buf.actions.data_ptr(), buf.rewards.data_ptr(),
+                              buf.episode_starts.data_ptr())
+        fb, ab, rb = n * F16_OBS_DIM * 4, n * 16, n * 4
+        L = lib()
+        boot = L.f16env_bootstrap_timeouts
         for t in range(T):
-            act = None
+            act_ptr = None
             if policy_fn is not None:
                 act, v, lp = policy_fn(obs)
+                if not (act.dtype == torch.float32 and act.is_contiguous() and act.shape == (n, 4)
+                        and act.device == dev and act.data_ptr() % 16 == 0):
+                    act = act.reshape(n, 4).to(device=dev, dtype=torch.float32).contiguous()
+                    if act.data_ptr() % 16:
+                        act = act.clone()
+                act_ptr = act.data_ptr()
                 buf.values[t].copy_(v.reshape(-1))
                 buf.log_probs[t].copy_(lp.reshape(-1))
-            nxt = buf.episode_starts[t + 1] if t + 1 < T else carry
-            frame_kw = ({"next_frame": buf.frames[t + 1] if t + 1 < T else None} if window
-                        else {"frame": buf.frames[t]})
-            out = envs.step_rollout(seed, step0 + t, actions=buf.actions[t], rewards=buf.rewards[t], next_start=nxt,
-                                    policy_actions=act, clip=policy_fn is not None, **frame_kw)
+            if raw:
+                slot.act_step = (int(step0) + t) & 0xFFFFFFFFFFFFFFFF
+                if window:
+                    slot.next_frame = fr0 + (t + 1) * fb if t + 1 < T else None
+                else:
+                    slot.frame = fr0 + t * fb
+                slot.actions, slot.rewards = ac0 + t * ab, rw0 + t * rb
+                slot.next_start = st0 + (t + 1) * rb if t + 1 < T else carry.data_ptr()
+                out = envs._step_rollout_raw(slot, act_ptr)
+            else:
+                nxt = buf.episode_starts[t + 1] if t + 1 < T else carry
+                frame_kw = ({"next_frame": buf.frames[t + 1] if t + 1 < T else None} if window
+                            else {"frame": buf.frames[t]})
+                out = envs.step_rollout(seed, step0 + t, actions=buf.actions[t], rewards=buf.rewards[t],
+                                        next_start=nxt, policy_actions=act if policy_fn is not None else None,
+                                        clip=policy_fn is not None, **frame_kw)
             if policy_fn is not None:  # timeout bootstrap on the step's terminal observations
                 tv = vfn(out.terminal_obs).reshape(-1).to(torch.float32).contiguous()
-                check(lib().f16env_bootstrap_timeouts(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n,
-                                                      buf.rewards[t].data_ptr(), out.terminated.data_ptr(),
-                                                      out.truncated.data_ptr(), tv.data_ptr(), buf.gamma),
+                check(boot(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n, rw0 + t * rb,
+                           out.terminated.data_ptr(), out.truncated.data_ptr(), tv.data_ptr(), buf.gamma),
                       "f16env_bootstrap_timeouts")
             obs = out.obs
         buf.pos = T

@@ -685,3 +685,33 @@ def test_host_checks_refuse_misshaped_buffers(torch_mod):
     out = g.step(a, done_idx=torch.zeros(n, **i32), n_done=torch.zeros(1, **i32))
     assert torch.isfinite(out.obs).all()
     g.close()
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "window"])
+def test_obs_bounds_counted_in_persistent_rollout(torch_mod, layout):
+    """F16_FLAG_OBS_CHECK in the one-launch rollout (f16_rollout_kernel counts its frames the way
+    the step kernel does): the same lane-steps as the oracle stepping the same
+    Philox actions, with a seventh of the lanes given an underground goal."""
+    torch = torch_mod
+    from f16_jsb_amd.abi import F16_FLAG_OBS_CHECK, F16C_GOAL
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout
+    n, T = 512, 20
+    ref = OracleEnvs(n, stack_k=4, seed=9, flags=F16_FLAG_OBS_CHECK)
+    g = F16Envs(n, stack_k=4, seed=9, obs_check=True, obs_layout=layout)
+    o = ref.reset()
+    g.reset()
+    s = ref.get_state()
+    bad = np.arange(n) % 7 == 0
+    s[bad, F16C_GOAL + 2] = -100.0
+    o[bad, :, 14] = -100.0
+    ref.set_state(s)
+    g.set_state(s)
+    g.set_obs(torch.as_tensor(o))
+    collect_rollout(g, DeviceRolloutBuffer(T, n, 4, g.device), 2, step0=4)  # one persistent launch
+    for t in range(T):
+        ref.step(ref.sample_actions(2, 4 + t))
+    assert ref.obs_bounds_count > 0
+    assert g.obs_bounds_count == ref.obs_bounds_count
+    ref.close()
+    g.close()

@@ -136,7 +136,7 @@ def test_cfg3_headline_instance_65536(torch_mod, layout, done_list):
     from f16_jsb_amd.env import F16Envs
     n = 65536
     ref, g = OracleEnvs(n, stack_k=4, seed=31), F16Envs(n, stack_k=4, seed=31, obs_layout=layout)
-    want = "f16_step_win_nt_kernel<0, 1>" if layout == "window" else "f16_step_kernel"
+    want = "f16_step_win_nt_kernel<0, 1, false>" if layout == "window" else "f16_step_kernel"
     assert g.step_kernel_name == want and g.waves_per_simd == 1, g.step_kernel_name
     o = ref.reset()
     o_g = g.reset().cpu().numpy()
@@ -161,7 +161,7 @@ def test_cfg5_production_instance_131072(torch_mod, layout, done_list):
     n = 131072
     ref = OracleEnvs(n, stack_k=4, seed=41, cfg5=True)
     g = F16Envs(n, stack_k=4, seed=41, cfg5=True, obs_layout=layout)
-    want = "f16_step_win_nt_kernel<3, 2>" if layout == "window" else "f16_step_var_kernel<3, 2, false>"
+    want = "f16_step_win_nt_kernel<3, 2, false>" if layout == "window" else "f16_step_var_kernel<3, 2, false>"
     assert g.step_kernel_name == want, g.step_kernel_name
     assert g.waves_per_simd == 2
     o = ref.reset()
@@ -199,7 +199,7 @@ def test_cfg5_inline_runic_resets_131072(torch_mod):
     n = 131072
     ref = OracleEnvs(n, stack_k=4, seed=43, cfg5=True, max_steps=5)
     g = F16Envs(n, stack_k=4, seed=43, cfg5=True, max_steps=5, obs_layout="window")
-    assert g.step_kernel_name == "f16_step_win_nt_kernel<3, 2>", g.step_kernel_name
+    assert g.step_kernel_name == "f16_step_win_nt_kernel<3, 2, false>", g.step_kernel_name
     o = ref.reset()
     g.reset()
     _stagger(ref, g, o, every=1, span=5)  # phases spread over the 5 steps; the next step refills the cache

@@ -83,7 +83,7 @@ def test_window_matches_contiguous(gpu, k, T, n, max_steps):
 def test_window_headline_size(gpu):
     """BASELINE cfg3 size (65 536 envs, K = 4): the one-wave window kernel over a restart."""
     a, b = _pair(65536, 4, 16, max_steps=1200)
-    assert b.step_kernel_name == "f16_step_win_nt_kernel<0, 1>"
+    assert b.step_kernel_name == "f16_step_win_nt_kernel<0, 1, false>"
     _run(a, b, 20, validity=False)
 
 
@@ -106,7 +106,7 @@ def test_window_cfg5_deferred_resets(gpu, monkeypatch, period):
     miscompile, see tests/test_isa_lint.py.)"""
     monkeypatch.setenv("F16ENV_ICC_PERIOD", period)
     a, b = _pair(512, 4, 8, max_steps=5, cfg5=True)
-    assert b.step_kernel_name == "f16_step_win_nt_kernel<3, 1>"
+    assert b.step_kernel_name == "f16_step_win_nt_kernel<3, 1, false>"
     assert _run(a, b, 30) > 512
 
 
@@ -160,15 +160,16 @@ def test_window_reset_then_set_state_keeps_fresh(gpu, cfg5):
 
 def test_window_views_and_layout(gpu):
     """The observation is a strided view of position-major 64-B frame slots: (N, K, 15), strides
-    (16, N*16, 1), the slots' 16th float 0; the rollout entry points refuse the window layout."""
-    from f16_jsb_amd.env import F16EnvError, F16Envs
+    (16, N*16, 1), the slots' 16th float 0. (The rollout entry points take the window layout since
+    round 4, tests/test_gpu_policy_rollout.py; their buffers are checked before any launch.)"""
+    from f16_jsb_amd.env import F16Envs
     e = F16Envs(64, stack_k=4, seed=1, obs_layout="window", history=16)
     o = e.reset()
     assert tuple(o.shape) == (64, 4, 15) and o.stride() == (16, 64 * 16, 1)
     for t in range(1, 30):  # across a restart
         e.step(e.sample_actions(1, t))
     assert float(e._hist[..., 15].abs().max()) == 0.0
-    with pytest.raises(F16EnvError):
+    with pytest.raises(ValueError):
         e.rollout_random(0, 0, 2, None, None, None, None, None)
 
 
