@@ -236,6 +236,39 @@ class MlpActorCritic:
         return act, self.value(obs), logp
 
 
+class GraphedPolicy:
+    """A policy's forward and value forward each captured once as a HIP graph (torch.cuda.graph:
+    hipStreamBeginCapture underneath) on a static (N, K, 15) input: per call one copy of the
+    observation (the window view, strided) into the static input and one graph replay, instead
+    of ~20 eagerly launched small kernels. The outputs are the graph's static tensors, valid
+    until the next call (collect_rollout consumes them within the step, in stream order)."""
+
+    def __init__(self, net, n, k, dev):
+        import torch
+        self.x = torch.zeros((n, k, 15), dtype=torch.float32, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                net(self.x), net.value(self.x)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.g, self.gv = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g):
+            self.out = net(self.x)
+        with torch.cuda.graph(self.gv):
+            self.vout = net.value(self.x)
+
+    def __call__(self, obs):
+        self.x.copy_(obs)
+        self.g.replay()
+        return self.out
+
+    def value(self, obs):
+        self.x.copy_(obs)
+        self.gv.replay()
+        return self.vout
+
+
 def rollout_bench(args, dev, rank, world):
     """BASELINE cfg4 beside the headline: a PPO-shaped rollout (n_steps x envs per GPU) into
     the device rollout buffer, HIP GAE, then the RCCL gather of every shard to rank 0.
@@ -314,36 +347,46 @@ def rollout_bench(args, dev, rank, world):
         sync()
         cont = {"rollout_fused_contiguous_s": round(time.perf_counter() - tc0, 4)}
         ec.close()
-    # policy in the loop (on_policy_algorithm.py:194-262 with a policy network)
+    # policy in the loop (on_policy_algorithm.py:194-262 with a policy network), eager and with
+    # the policy's forwards captured as HIP graphs
     pol = {}
     if args.policy_steps > 0:
         net = MlpActorCritic(args.stack * 15, dev, seed=args.seed)
         pbuf = DeviceRolloutBuffer(args.policy_steps, n, args.stack, dev)
-        with torch.no_grad():
-            collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), policy_fn=net, value_fn=net.value)
+
+        def policy_leg(pf, vf):
+            collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), policy_fn=pf, value_fn=vf)
             barrier()
             tq0 = time.perf_counter()
-            lv, ld = collect_rollout(envs, pbuf, policy_fn=net, value_fn=net.value)
+            lv, ld = collect_rollout(envs, pbuf, policy_fn=pf, value_fn=vf)
             pbuf.compute_returns_and_advantage(lv, ld)
             sync()
             pol_s = time.perf_counter() - tq0
-            # the policy's share: its forward + the terminal-value forward alone, same batch
-            o = envs.obs
+            o = envs.obs  # the policy's share: its forward + the value forward alone, same batch
             for _ in range(3):
-                net(o), net.value(o)
+                pf(o), vf(o)
             sync()
             tq1 = time.perf_counter()
             for _ in range(50):
-                net(o), net.value(o)
+                pf(o), vf(o)
             sync()
-            policy_ms = (time.perf_counter() - tq1) / 50 * 1e3
+            return {"rollout_plus_gae_s": round(pol_s, 4),
+                    "env_steps_per_s": round(n * world * args.policy_steps / pol_s, 1),
+                    "ms_per_step": round(pol_s / args.policy_steps * 1e3, 5),
+                    "policy_forward_ms_per_step": round((time.perf_counter() - tq1) / 50 * 1e3, 5)}
+
+        with torch.no_grad():
+            eager = policy_leg(net, net.value)
+            gp = GraphedPolicy(net, n, args.stack, dev)
+            graphed = policy_leg(gp, gp.value)
         pol = {"policy_in_the_loop": {
-            "policy": "MlpActorCritic (SB3 default PPO MlpPolicy shape: pi/vf [64, 64] tanh, Gaussian, random init), "
-                      "torch eager on the window view, actions clipped in-kernel, timeout bootstrap on device",
-            "steps": args.policy_steps, "rollout_plus_gae_s": round(pol_s, 4),
-            "env_steps_per_s": round(n * world * args.policy_steps / pol_s, 1),
-            "ms_per_step": round(pol_s / args.policy_steps * 1e3, 5),
-            "policy_forward_ms_per_step": round(policy_ms, 5)}}
+            "policy": "MlpActorCritic (SB3 default PPO MlpPolicy shape: pi/vf [64, 64] tanh, Gaussian, random init) "
+                      "on the window view; actions clipped in-kernel, timeout bootstrap on device "
+                      "(f16env_window_step_rollout + f16env_bootstrap_timeouts), then GAE",
+            "steps": args.policy_steps, **graphed,
+            "policy_execution": "forward and value forward each captured as a HIP graph (torch.cuda.graph), "
+                                "one replay per call",
+            "eager": eager}}
         del pbuf
     gathered = 0
     t_gather = 0.0

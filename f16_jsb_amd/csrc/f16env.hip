@@ -562,6 +562,7 @@ struct StepArgs {
   int64_t wrow;                // floats between positions (position-major: N * 16; env-major: 16)
   int64_t wenv;                // floats between envs (position-major: 16; env-major: T * 16)
   int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
+  int32_t half_delay;          // HALF builds (experiment): cycles the second half of the grid waits
   // cfg5 modes, windowed layout: the reset cache (f16_ic_fill_kernel): per lane the state and
   // frame 0 (without the goal) of its NEXT reset, ICC_COLS columns; c == nullptr: deferred
   // resets by f16_reset_done_kernel instead
@@ -620,20 +621,30 @@ struct StepPre {
   const float4* tmpl;
   int64_t n;
 };
-template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false>
+// HALF (windowed builds, an experiment: F16ENV_HALF=1): 32 envs per wave in lanes 0-31, so a
+// grid of N envs is N/32 waves -- two per SIMD at 65 536 envs -- and the second half of the
+// grid may start `half_delay` cycles late, so that one wave's memory phases (prologue loads,
+// store tail) overlap the other's frames on the same SIMD.
+template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false,
+          bool HALF = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl,
                                           const StepPre* pre = nullptr) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
+  constexpr int EPW = HALF ? 32 : 64;  // envs per wave
 #ifdef F16_STAMPS
   Stamps stamps = {};
   stamps.last = memtime();
 #endif
+  if (HALF && a.half_delay > 0 && blockIdx.x >= gridDim.x / 2) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)a.half_delay) __builtin_amdgcn_s_sleep(8);
+  }
   const int KC = a.E.K * F16_OBS_DIM, HC = (a.E.K - 1) * F16_OBS_DIM;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t row0 = (int64_t)blockIdx.x * BLOCK + wave * 64;
+  const int64_t row0 = (int64_t)blockIdx.x * (4 * EPW) + wave * EPW;
   const int64_t nE = pre ? pre->n : a.E.n;
-  const int rows = (int)(nE - row0 < 64 ? (nE - row0 > 0 ? nE - row0 : 0) : 64);
+  const int rows = (int)(nE - row0 < EPW ? (nE - row0 > 0 ? nE - row0 : 0) : EPW);
   const bool image = a.lds_image != 0;
   // cfg5 modes in the windowed layout reset finished lanes in the step (reset cache)
   const bool in_step_reset = WIN && DEFER && a.icc.c != nullptr && !(a.E.flags & F16_FLAG_NO_AUTORESET);
@@ -656,8 +667,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (lane < (total & 3)) dma4(prev + 4 * n16 + lane, img + IMG_OFF + 4 * n16);  // tail, never past the end
     }
   };
-  const int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = k < nE;
+  const int64_t k = row0 + lane;
+  const bool live = (!HALF || lane < EPW) && k < nE;
   F16_CHECK(rows >= 0 && rows <= 64 && (!live || row0 + lane < nE), DBG_STATE_INDEX);
   if (WIN) F16_CHECK(a.wpos >= a.E.K - 1 && a.wpos >= 0, DBG_WINDOW_POS);
   int done = 0;
@@ -897,7 +908,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     // store instruction writes 1 KiB contiguous (16 whole slots, 4 lanes per slot) instead of a
     // 16-B quarter of every slot. Swizzle: quarter j of slot r at float4 r*4 + (j ^ (r>>2 & 3)),
     // conflict-free on both the per-lane writes and the per-slot reads.
-    if (rows == 64) {
+    if (rows == EPW) {
       float4* st4 = reinterpret_cast<float4*>(stg);
       const int q = lane & 3, sw = (lane >> 2) & 3;
       float* const hist[2] = {a.wx, a.wy};
@@ -912,31 +923,27 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         __builtin_amdgcn_wave_barrier();
         float* dst = hist[h] + (int64_t)p * a.wrow + (row0 + (lane >> 2)) * a.wenv + 4 * q;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < EPW / 16; ++j) {
           const int r = 16 * j + (lane >> 2);
           st16<NT>(reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * a.wenv), st4[r * 4 + (q ^ ((r >> 2) & 3))]);
         }
         if (ROLL && h == 0 && a.r_next_frame) {
           // the rollout's frame log: the returned observation's newest frame (the next slot's
-          // frame), the wave's 64 rows as 960 contiguous floats = 240 float4 from the same
-          // staging (element c of slot r at float4 r*4 + ((c>>2) ^ sw(r)), component c & 3);
-          // a log whose rows are not 16-B aligned (N % 4 != 0) takes dword stores
-          const float* sf = reinterpret_cast<const float*>(st4);
+          // frame), the wave's 64 rows as 960 contiguous floats: each lane writes its 15 floats
+          // at a 15-float pitch into the (now free) staging area (odd pitch: conflict-free),
+          // then 240 float4 go out linearly; a log whose rows are not 16-B aligned (N % 4 != 0)
+          // takes dword stores
+          float* sf = reinterpret_cast<float*>(st4);
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int c = 0; c < F16_OBS_DIM; ++c) sf[lane * F16_OBS_DIM + c] = fr[c];
+          __builtin_amdgcn_wave_barrier();
           float* dstf = a.r_next_frame + row0 * F16_OBS_DIM;
-          const bool al = ((uintptr_t)dstf & 15) == 0;
-          for (int u = lane; u < 64 * F16_OBS_DIM / 4; u += 64) {
-            float v[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int e = 4 * u + i, r = e / F16_OBS_DIM, c = e - r * F16_OBS_DIM;
-              v[i] = sf[(r * 4 + ((c >> 2) ^ ((r >> 2) & 3))) * 4 + (c & 3)];
-            }
-            if (al) {
-              reinterpret_cast<float4*>(dstf)[u] = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
-#pragma unroll
-              for (int i = 0; i < 4; ++i) dstf[4 * u + i] = v[i];
-            }
+          if (((uintptr_t)dstf & 15) == 0) {
+            for (int u = lane; u < 64 * F16_OBS_DIM / 4; u += 64)
+              reinterpret_cast<float4*>(dstf)[u] = reinterpret_cast<const float4*>(sf)[u];
+          } else {
+            for (int u = lane; u < 64 * F16_OBS_DIM; u += 64) dstf[u] = sf[u];
           }
         }
       }
@@ -1120,6 +1127,16 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(const float
   STEP_SHARED
   const StepPre pre = {sc, act, tmpl, n};
   step_body<MODE, false, ROLL, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
+}
+// the half-populated-wave experiment (HALF above): 256-register build, two waves per SIMD
+template <int MODE>
+__global__ __launch_bounds__(BLOCK, 2) void f16_step_win_half_kernel(const float4* __restrict__ sc,
+                                                                     const float* __restrict__ act,
+                                                                     const float4* __restrict__ tmpl, int64_t n,
+                                                                     StepArgs a) {
+  STEP_SHARED
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, false, false, true, true, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
 using StepKernel = void (*)(const float4*, const float*, const float4*, int64_t, StepArgs);
 using WinKernel = StepKernel;
@@ -1890,6 +1907,8 @@ struct f16env {
   int win_occ;        // the same for the windowed-observation step kernel
   int win_env_major;  // window histories [N][T][16] (1) instead of the default [T][N][16] (0)
   int win_nt;         // windowed step: non-temporal output stores
+  int win_half;       // experiment (F16ENV_HALF=1): 32 envs per wave, f16_step_win_half_kernel
+  int half_delay;     // ... and the second half of its grid starting this many cycles late
   struct {            // f16env_window_bind: the buffers of f16env_window_step_bound
     float* hist[2];
     int64_t T;
@@ -2080,6 +2099,8 @@ int f16env_create(const f16env_config* cfg, int device, f16env_t* out) {
     // once (one round of waves); with more rounds they cost (st16)
     h->win_nt = waves <= (int64_t)h->win_occ * 4 * cus ? 1 : 0;
     if (getenv("F16ENV_WIN_NT")) h->win_nt = atoi(getenv("F16ENV_WIN_NT")) ? 1 : 0;
+    h->win_half = getenv("F16ENV_HALF") ? (atoi(getenv("F16ENV_HALF")) ? 1 : 0) : 0;
+    h->half_delay = getenv("F16ENV_HALF_DELAY") ? atoi(getenv("F16ENV_HALF_DELAY")) : 0;
     for (int v = 0; v <= 2; ++v) {
       const size_t st_v = v == 2 ? static_gt : static_lds;
       for (int m = 0; m < 8; ++m) {
@@ -2396,7 +2417,7 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
   a.lds_image = 0;
   hipStream_t st = (hipStream_t)stream;
   int32_t* zero_next = nullptr;
-  const dim3 grid(nblocks(a.E.n)), blk(BLOCK);
+  const dim3 blk(BLOCK);
   // cfg5 modes: finished lanes are reset inside the step from the reset cache (period 0 or
   // F16ENV_ICC_PERIOD=0: the deferred f16_reset_done_kernel instead)
   const bool cache = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period > 0;
@@ -2409,7 +2430,15 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
   } else if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) {
     return e;
   }
-  const WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt, slot != nullptr);
+  WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt, slot != nullptr);
+  dim3 grid(nblocks(a.E.n));
+  if (h->win_half && !slot) {  // the half-populated-wave experiment: 128 envs per block
+    static const WinKernel half[4] = {f16_step_win_half_kernel<0>, f16_step_win_half_kernel<1>,
+                                      f16_step_win_half_kernel<2>, f16_step_win_half_kernel<3>};
+    kern = half[h->mode & 3];
+    grid = dim3((unsigned)((a.E.n + 127) / 128));
+    a.half_delay = h->half_delay;
+  }
   const float4* sc = a.s.c;
   const float4* tc = a.tmpl.c;
   const int64_t n = a.E.n;
