@@ -869,7 +869,8 @@ def main():
             # (BASELINE.json); the kernel itself is latency-bound: one wave per SIMD at 65 536 envs,
             # neither HBM (frac) nor VALU issue (valu.valu_busy_frac) saturated
             "bound": "hbm",
-            "limiter": "latency (one wave per SIMD: neither HBM nor VALU issue saturated)",
+            "limiter": ("latency (%s per SIMD: neither HBM nor VALU issue saturated)"
+                        % ("one wave" if waves_per_simd == 1 else "%d waves" % waves_per_simd)),
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
