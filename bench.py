@@ -775,9 +775,12 @@ def main():
         envs.step(acts[t % pool])
     end_ev.record(stream)
     torch.cuda.synchronize()
+    # each rank's own K steps, barrier to barrier; the job's time is the max over ranks (all_reduce
+    # below). The closing barrier stays outside the clock: its collective latency (tens of us on
+    # RCCL) is not stepping, and a 20-step region would carry it as ~1-2 us per step at N > 1 only
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     gc.enable()
     gpu_ms_per_step = start_ev.elapsed_time(end_ev) / args.steps
     # auto-resets inside the timed region, from the lanes' episode counters (read after it:
