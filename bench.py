@@ -245,6 +245,7 @@ class GraphedPolicy:
 
     def __init__(self, net, n, k, dev):
         import torch
+        self.net, self.n = net, n
         self.x = torch.zeros((n, k, 15), dtype=torch.float32, device=dev)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -264,6 +265,8 @@ class GraphedPolicy:
         return self.out
 
     def value(self, obs):
+        if obs.shape[0] != self.n:  # another batch (the deferred bootstrap's stash): eager
+            return self.net.value(obs)
         self.x.copy_(obs)
         self.gv.replay()
         return self.vout
@@ -354,38 +357,50 @@ def rollout_bench(args, dev, rank, world):
         net = MlpActorCritic(args.stack * 15, dev, seed=args.seed)
         pbuf = DeviceRolloutBuffer(args.policy_steps, n, args.stack, dev)
 
-        def policy_leg(pf, vf):
-            collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), policy_fn=pf, value_fn=vf)
+        def policy_leg(pf, vf, bootstrap="deferred"):
+            collect_rollout(envs, DeviceRolloutBuffer(8, n, args.stack, dev), policy_fn=pf, value_fn=vf,
+                            bootstrap=bootstrap)
             barrier()
             tq0 = time.perf_counter()
-            lv, ld = collect_rollout(envs, pbuf, policy_fn=pf, value_fn=vf)
+            lv, ld = collect_rollout(envs, pbuf, policy_fn=pf, value_fn=vf, bootstrap=bootstrap)
             pbuf.compute_returns_and_advantage(lv, ld)
             sync()
             pol_s = time.perf_counter() - tq0
-            o = envs.obs  # the policy's share: its forward + the value forward alone, same batch
+            o = envs.obs  # the policy's share: its forward (and the value forward) alone, same batch
             for _ in range(3):
                 pf(o), vf(o)
             sync()
             tq1 = time.perf_counter()
             for _ in range(50):
-                pf(o), vf(o)
+                pf(o)
             sync()
+            tq2 = time.perf_counter()
+            for _ in range(50):
+                vf(o)
+            sync()
+            tq3 = time.perf_counter()
             return {"rollout_plus_gae_s": round(pol_s, 4),
                     "env_steps_per_s": round(n * world * args.policy_steps / pol_s, 1),
                     "ms_per_step": round(pol_s / args.policy_steps * 1e3, 5),
-                    "policy_forward_ms_per_step": round((time.perf_counter() - tq1) / 50 * 1e3, 5)}
+                    "policy_forward_ms": round((tq2 - tq1) / 50 * 1e3, 5),
+                    "value_forward_ms": round((tq3 - tq2) / 50 * 1e3, 5)}
 
         with torch.no_grad():
             eager = policy_leg(net, net.value)
             gp = GraphedPolicy(net, n, args.stack, dev)
             graphed = policy_leg(gp, gp.value)
+            graphed_per_step = policy_leg(gp, gp.value, bootstrap="per_step")
         pol = {"policy_in_the_loop": {
             "policy": "MlpActorCritic (SB3 default PPO MlpPolicy shape: pi/vf [64, 64] tanh, Gaussian, random init) "
-                      "on the window view; actions clipped in-kernel, timeout bootstrap on device "
-                      "(f16env_window_step_rollout + f16env_bootstrap_timeouts), then GAE",
+                      "on the window view; actions clipped in-kernel, timeout bootstrap on device, deferred: "
+                      "truncated lanes' terminal observations stashed per step, V once after the loop "
+                      "(f16env_window_step_rollout + f16env_bootstrap_stash / _apply), then GAE",
             "steps": args.policy_steps, **graphed,
             "policy_execution": "forward and value forward each captured as a HIP graph (torch.cuda.graph), "
-                                "one replay per call",
+                                "one replay per call (the deferred bootstrap's value call over the stash: eager)",
+            "bootstrap_per_step": {**graphed_per_step,
+                                   "note": "V over the whole batch of terminal observations every step "
+                                           "(f16env_bootstrap_timeouts), as round 4's first version"},
             "eager": eager}}
         del pbuf
     gathered = 0

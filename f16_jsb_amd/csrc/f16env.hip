@@ -2681,6 +2681,72 @@ int f16env_bootstrap_timeouts(void* stream, int64_t n, float* rewards, const uin
   return 0;
 }
 
+// The deferred timeout bootstrap (include/f16env.h): per step, the terminal observations of the
+// lanes that ended by truncation alone are appended to a stash (one atomic per wave, ballot
+// compaction as the step kernel's done list); after the rollout one value evaluation over the
+// stash and a scatter of gamma * V into the rewards.
+__global__ __launch_bounds__(256) void f16_bootstrap_stash_kernel(int64_t n, int32_t K, const float* __restrict__ tobs,
+                                                                  int64_t row_stride, int64_t frame_stride,
+                                                                  const uint8_t* __restrict__ term,
+                                                                  const uint8_t* __restrict__ trunc, int64_t flat_base,
+                                                                  float* __restrict__ stash, int64_t* __restrict__ idx,
+                                                                  int32_t* count, int64_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool take = i < n && trunc[i] && !term[i];
+  const unsigned long long m = __ballot(take);
+  if (!m) return;  // wave-uniform
+  int base = 0;
+  if (lane == 0) base = atomicAdd(count, __popcll(m));
+  base = __shfl(base, 0);
+  if (!take) return;
+  const int64_t slot = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+  F16_CHECK(slot >= 0, DBG_DONE_LIST);
+  if (slot >= cap) return;
+  float* dst = stash + slot * (int64_t)K * F16_OBS_DIM;
+  for (int j = 0; j < K; ++j) {
+    const float* src = tobs + i * row_stride + (int64_t)j * frame_stride;
+#pragma unroll
+    for (int c = 0; c < F16_OBS_DIM; ++c) dst[j * F16_OBS_DIM + c] = src[c];
+  }
+  idx[slot] = flat_base + i;
+}
+
+__global__ void f16_bootstrap_apply_kernel(int64_t m, float* __restrict__ rew, const int64_t* __restrict__ idx,
+                                           const float* __restrict__ v, float g) {
+#pragma clang fp contract(off)
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int64_t r = idx[j];
+  rew[r] = rew[r] + g * v[j];
+}
+
+int f16env_bootstrap_stash(void* stream, int64_t n, int32_t K, const float* tobs, int64_t row_stride,
+                           int64_t frame_stride, const uint8_t* terminated, const uint8_t* truncated,
+                           int64_t flat_base, float* stash_obs, int64_t* stash_idx, int32_t* count,
+                           int64_t capacity) {
+  if (n < 0 || K < 1 || capacity < 0) return set_err(-1, "n >= 0, K >= 1 and capacity >= 0 required");
+  if (n == 0) return 0;
+  if (!tobs || !terminated || !truncated || !stash_idx || !count || (capacity > 0 && !stash_obs))
+    return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_bootstrap_stash_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     n, K, tobs, row_stride, frame_stride, terminated, truncated, flat_base, stash_obs, stash_idx,
+                     count, capacity);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_bootstrap_apply(void* stream, int64_t m, float* rewards, const int64_t* idx, const float* values,
+                           double gamma) {
+  if (m < 0) return set_err(-1, "m must be >= 0");
+  if (m == 0) return 0;
+  if (!rewards || !idx || !values) return set_err(-1, "null argument");
+  hipLaunchKernelGGL(f16_bootstrap_apply_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     m, rewards, idx, values, (float)gamma);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int f16env_abi_version(void) { return F16ENV_ABI_VERSION; }
 
 int f16env_get_state(f16env_t h, void* stream, double* canon) {

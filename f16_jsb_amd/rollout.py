@@ -106,7 +106,7 @@ def np_clip_actions(a):
 
 
 def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 0, policy_fn=None, value_fn=None,
-                    fused: bool = True, persistent: bool = True):
+                    fused: bool = True, persistent: bool = True, bootstrap: str = "deferred"):
     """collect_rollouts (on_policy_algorithm.py:162-268) over device tensors. Starts from the
     envs' current observation; returns (last_values, last_dones) for GAE (:258-262).
 
@@ -126,7 +126,15 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
     buffer copies (RolloutBuffer.add, buffers.py:440-479).
     persistent (no policy_fn): the whole rollout is ONE launch (f16env_rollout_random /
     f16env_window_rollout_random) that keeps every env's state on-chip across the steps:
-    bit-identical to the fused launches."""
+    bit-identical to the fused launches.
+    bootstrap "deferred" (fused path, auto-resetting handles): the terminal observations of the
+    lanes that end by truncation alone are appended to a device stash after each step
+    (f16env_bootstrap_stash, no host sync) and V runs ONCE over the stash after the loop
+    (f16env_bootstrap_apply scatters gamma * V into the rewards) -- the value network does not
+    change during a rollout, so this is :236-245's arithmetic with one evaluation instead of one
+    per step over the whole batch; "per_step": V over the step's whole batch of terminal
+    observations every step (f16env_bootstrap_timeouts). The two agree bit for bit when V's value
+    for a row does not depend on the batch it is evaluated in."""
 
     dev = buf.device
     n = buf.n_envs
@@ -172,6 +180,18 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
         fb, ab, rb = n * F16_OBS_DIM * 4, n * 16, n * 4
         L = lib()
         boot = L.f16env_bootstrap_timeouts
+        defer = policy_fn is not None and bootstrap == "deferred" \
+            and not (int(getattr(envs, "cfg").flags) & F16_FLAG_NO_AUTORESET)
+        if bootstrap not in ("deferred", "per_step"):
+            raise ValueError("bootstrap must be 'deferred' or 'per_step'")
+        if defer:
+            # a lane truncates at most once per max_steps steps (auto-reset restarts its counter),
+            # so it enters the stash at most (T - 1) // max_steps + 1 times in T steps
+            cap = n * ((T - 1) // max(1, int(envs.cfg.max_steps)) + 1)
+            stash = torch.empty((cap, buf.k, F16_OBS_DIM), dtype=torch.float32, device=dev)
+            stash_idx = torch.empty(cap, dtype=torch.int64, device=dev)
+            stash_n = torch.zeros(1, dtype=torch.int32, device=dev)
+            stash_fn = L.f16env_bootstrap_stash
         for t in range(T):
             act_ptr = None
             if policy_fn is not None:
@@ -200,12 +220,27 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
                 out = envs.step_rollout(seed, step0 + t, actions=buf.actions[t], rewards=buf.rewards[t],
                                         next_start=nxt, policy_actions=act if policy_fn is not None else None,
                                         clip=policy_fn is not None, **frame_kw)
-            if policy_fn is not None:  # timeout bootstrap on the step's terminal observations
+            if defer:  # the truncated lanes' terminal observations into the stash
+                tobs = out.terminal_obs
+                check(stash_fn(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n, buf.k, tobs.data_ptr(),
+                               tobs.stride(0), tobs.stride(1), out.terminated.data_ptr(), out.truncated.data_ptr(),
+                               t * n, stash.data_ptr(), stash_idx.data_ptr(), stash_n.data_ptr(), cap),
+                      "f16env_bootstrap_stash")
+            elif policy_fn is not None:  # timeout bootstrap on the step's terminal observations
                 tv = vfn(out.terminal_obs).reshape(-1).to(torch.float32).contiguous()
                 check(boot(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n, rw0 + t * rb,
                            out.terminated.data_ptr(), out.truncated.data_ptr(), tv.data_ptr(), buf.gamma),
                       "f16env_bootstrap_timeouts")
             obs = out.obs
+        if defer:  # V once over every stashed terminal observation, then rewards += gamma * V
+            m = int(stash_n.item())
+            if m > cap:
+                raise RuntimeError("bootstrap stash overflow (%d > %d)" % (m, cap))
+            if m:
+                tv = vfn(stash[:m]).reshape(-1).to(torch.float32).contiguous()
+                check(L.f16env_bootstrap_apply(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), m, rw0,
+                                               stash_idx.data_ptr(), tv.data_ptr(), buf.gamma),
+                      "f16env_bootstrap_apply")
         buf.pos = T
         starts = carry
     else:

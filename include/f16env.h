@@ -27,6 +27,8 @@
  *   f16env_rollout_random / f16env_window_rollout_random <- on_policy_algorithm.py:194-262's
  *                      loop under the uniform random policy, one launch
  *   f16env_bootstrap_timeouts <- on_policy_algorithm.py:236-245 (timeout bootstrap)
+ *   f16env_bootstrap_stash / f16env_bootstrap_apply <- the same, deferred to the end of the
+ *                      rollout (one value evaluation over the stashed terminal observations)
  *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
  *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
  *   f16env_poses    <- jsbsim_gym.py:381-415 JSBSimEnv.render state -> Viewer poses (8f rank 4)
@@ -44,7 +46,8 @@ extern "C" {
 /* 3 (round 4): f16env_step_kernel_name takes the handle (was (void)); f16env_set_state keeps the
  * windowed layout's FRESH mark; the rollout slot gained next_frame / flags (F16_SLOT_CLIP);
  * f16env_rollout_random has no stack_k / mode limits; new f16env_window_step_rollout,
- * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_abi_version. */
+ * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_bootstrap_stash,
+ * f16env_bootstrap_apply, f16env_abi_version. */
 #define F16ENV_ABI_VERSION 3
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
@@ -342,6 +345,25 @@ int f16env_window_rollout_random(f16env_t h, void* stream, uint64_t seed, uint64
  * SB3's rounding (f32(gamma) * v, then the sum). In place; stream-ordered; no handle needed. */
 int f16env_bootstrap_timeouts(void* stream, int64_t n, float* rewards, const uint8_t* terminated,
                               const uint8_t* truncated, const float* terminal_values, double gamma);
+
+/* The timeout bootstrap deferred to the end of a rollout. SB3 evaluates V(terminal_obs) lane by
+ * lane inside the step loop (on_policy_algorithm.py:236-245); the value network does not change
+ * during a rollout, so the evaluation can wait until the loop is done and run once over every
+ * terminal observation that needs it, instead of over the whole batch at every step.
+ * f16env_bootstrap_stash (once per step, after it): every lane i < n with truncated[i] &&
+ * !terminated[i] appends its terminal observation -- K frames of 15 floats, frame j at
+ * tobs + i * row_stride + j * frame_stride (floats; the contiguous (N, K, 15) layout or a window
+ * view) -- to stash_obs (capacity x K x 15) and flat_base + i to stash_idx, at a slot taken from
+ * *count (a wave-aggregated atomic add); slots at or past `capacity` are counted, not written
+ * (the caller checks *count <= capacity). f16env_bootstrap_apply (after the rollout):
+ * rewards[idx[j]] += f32(gamma) * values[j] for j < m (SB3's rounding, as
+ * f16env_bootstrap_timeouts), the idx distinct. */
+int f16env_bootstrap_stash(void* stream, int64_t n, int32_t K, const float* tobs, int64_t row_stride,
+                           int64_t frame_stride, const uint8_t* terminated, const uint8_t* truncated,
+                           int64_t flat_base, float* stash_obs, int64_t* stash_idx, int32_t* count,
+                           int64_t capacity);
+int f16env_bootstrap_apply(void* stream, int64_t m, float* rewards, const int64_t* idx, const float* values,
+                           double gamma);
 
 /* F16ENV_ABI_VERSION of the built library (a binding checks it against its header). */
 int f16env_abi_version(void);

@@ -87,7 +87,7 @@ def test_policy_rollout_cfg4_share_vs_oracle(gpu):
     _stagger(ref, g, o, span=25)  # a third of the lanes truncate inside the 30 steps
     policy, value, rec, vrec = _policy(gpu, g)
     buf = DeviceRolloutBuffer(T, N, K, gpu, gamma=GAMMA)
-    last_v, last_d = collect_rollout(g, buf, seed=SEED, policy_fn=policy, value_fn=value)
+    last_v, last_d = collect_rollout(g, buf, seed=SEED, policy_fn=policy, value_fn=value, bootstrap="per_step")
     torch.cuda.synchronize()
     assert len(rec) == T and len(vrec) == T + 1
     fr, ac, rw = buf.frames.cpu().numpy(), buf.actions.cpu().numpy(), buf.rewards.cpu().numpy()
@@ -133,6 +133,73 @@ def test_policy_rollout_cfg4_share_vs_oracle(gpu):
     np.testing.assert_array_equal(buf.returns.cpu().numpy(), ret)
     ref.close()
     g.close()
+
+
+def _elementwise_policy(dev, k):
+    """policy(obs) and value(obs) whose value for a row does not depend on the batch it is
+    evaluated in (a fixed-order elementwise sum, no GEMM): the deferred bootstrap evaluates V over
+    the stashed terminal observations, the per-step one over the whole batch every step."""
+    import torch
+    rng = np.random.default_rng(23)
+    W = torch.as_tensor(rng.normal(size=(9, 4)).astype(np.float32) * 0.7, device=dev)
+    wv = [float(x) for x in rng.normal(size=9).astype(np.float32)]
+
+    def feats(obs):
+        x = obs[:, -1, :]
+        return [x[:, 4] * 8, x[:, 5] * 8, x[:, 6], x[:, 7], x[:, 8], x[:, 9], x[:, 10], (x[:, 2] - 1500.0) / 3000.0,
+                x[:, 3] - 0.8]
+
+    def value(obs):
+        f = feats(obs)
+        v = f[0] * wv[0]
+        for j in range(1, 9):
+            v = v + f[j] * wv[j]
+        return v
+
+    def policy(obs):
+        z = torch.stack(feats(obs), 1)
+        a = (z @ W + torch.tensor([0.0, 0.1, 0.0, 0.5], device=dev)).contiguous()
+        return a, value(obs), -(a * a).sum(1)
+
+    return policy, value
+
+
+@pytest.mark.parametrize("layout,k", [("window", 4), ("contiguous", 4), ("window", 10)])
+def test_deferred_bootstrap_equals_per_step(gpu, layout, k):
+    """The deferred timeout bootstrap (terminal observations of truncated lanes stashed on device
+    per step, one V evaluation after the rollout, f16env_bootstrap_stash / _apply) against the
+    per-step one (V over the whole batch every step, f16env_bootstrap_timeouts): with a value head
+    whose rows do not depend on the batch, every buffer -- rewards included -- and the last values
+    are bit-identical, over two consecutive rollouts at cfg4's share with staggered truncations
+    (and every lane truncating several times with a 9-step TimeLimit in the K = 10 case)."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout
+    N, T = 32768, 40
+    ms = 9 if k == 10 else 1200
+    runs = {}
+    for mode in ("per_step", "deferred"):
+        ref = OracleEnvs(N, stack_k=k, seed=61, max_steps=ms)
+        g = F16Envs(N, stack_k=k, seed=61, max_steps=ms, obs_layout=layout)
+        o = ref.reset()
+        g.reset()
+        _stagger(ref, g, o, span=min(25, ms))
+        ref.close()
+        policy, value = _elementwise_policy(gpu, k)
+        out = {}
+        for r in range(2):
+            buf = DeviceRolloutBuffer(T, N, k, gpu)
+            lv, ld = collect_rollout(g, buf, seed=61 + r, policy_fn=policy, value_fn=value, bootstrap=mode)
+            for f in ("frames", "actions", "rewards", "episode_starts", "values", "log_probs"):
+                out["%s%d" % (f, r)] = getattr(buf, f).clone()
+            out["last_v%d" % r], out["last_d%d" % r] = lv.clone(), ld.clone()
+        runs[mode] = out
+        g.close()
+    a, b = runs["per_step"], runs["deferred"]
+    for f in a:
+        assert torch.equal(a[f], b[f]), f
+    trunc_boot = int((a["episode_starts0"][1:] > 0).sum())
+    assert trunc_boot > N // 4, trunc_boot
 
 
 def _crash_ics(n):
