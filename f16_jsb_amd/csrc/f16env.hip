@@ -1712,8 +1712,7 @@ __global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t s
 // not depend on the chain, so they are software-pipelined: the rewards / values / starts of the
 // next block of U steps are issued before the current block is computed, keeping ~2U steps of
 // loads in flight per lane (round 3's loop waited on each step's three loads in turn: 0.13 of
-// HBM peak). LPW lanes of each 64-lane wave carry an env (LPW = 32: 1 024 half-populated waves
-// at 32 768 envs, one per SIMD, twice the memory requests in flight for the same bytes).
+// HBM peak). LPW lanes of each 64-lane wave carry an env (64: full waves, f16env_gae below).
 // Streaming data: non-temporal loads and stores.
 template <int U>
 __device__ __forceinline__ void gae_load(int64_t s0, int64_t n_envs, int64_t e, const float* __restrict__ rewards,
@@ -2802,18 +2801,25 @@ int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewar
   if (!rewards || !values || !episode_starts || !last_values || !dones || !advantages || !returns)
     return set_err(-1, "null argument");
   const float g = (float)gamma, gl = (float)(gamma * gae_lambda);
-  // half-populated waves while that still leaves >= one wave per SIMD's worth of envs idle
-  // otherwise (cfg4: 32 768 envs -> 1 024 waves); F16ENV_GAE_LPW=64|32 overrides
-  static const int lpw_env = getenv("F16ENV_GAE_LPW") ? atoi(getenv("F16ENV_GAE_LPW")) : 0;
-  const int lpw = lpw_env == 64 || lpw_env == 32 ? lpw_env : (n_envs <= 1024 * 32 ? 32 : 64);
+  // full waves and 32-step load blocks: at cfg4's 2 048 x 32 768, 0.236 ms (5.69 TB/s) against
+  // 0.266 with half-populated waves (1 024 waves, round 4's first version) and 0.29-0.30 with two
+  // envs per lane by float2 moves (tools/gae_sweep.py, profiles/r04_gae_sweep.json: per load
+  // instruction the full wave moves two 128-B lines instead of one). F16ENV_GAE_LPW=16|32|64 and
+  // F16ENV_GAE_U=8|16|32 select the others (A/B only).
+  static const int lpw_env = getenv("F16ENV_GAE_LPW") ? atoi(getenv("F16ENV_GAE_LPW")) : 64;
+  static const int u_env = getenv("F16ENV_GAE_U") ? atoi(getenv("F16ENV_GAE_U")) : 32;
+  const int lpw = lpw_env == 32 || lpw_env == 16 ? lpw_env : 64;
   const int64_t blocks = (n_envs + lpw - 1) / lpw;
   if (blocks > 0x7fffffffLL) return set_err(-1, "n_envs too large");
-  if (lpw == 32)
-    hipLaunchKernelGGL((f16_gae_kernel<16, 32>), dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, n_steps,
-                       n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
-  else
-    hipLaunchKernelGGL((f16_gae_kernel<16, 64>), dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, n_steps,
-                       n_envs, rewards, values, episode_starts, last_values, dones, g, gl, advantages, returns);
+  using GaeKernel = void (*)(int64_t, int64_t, const float*, const float*, const float*, const float*, const uint8_t*,
+                             float, float, float*, float*);
+  static const GaeKernel table[3][3] = {
+      {f16_gae_kernel<8, 16>, f16_gae_kernel<8, 32>, f16_gae_kernel<8, 64>},
+      {f16_gae_kernel<16, 16>, f16_gae_kernel<16, 32>, f16_gae_kernel<16, 64>},
+      {f16_gae_kernel<32, 16>, f16_gae_kernel<32, 32>, f16_gae_kernel<32, 64>}};
+  const GaeKernel kern = table[u_env == 8 ? 0 : (u_env == 16 ? 1 : 2)][lpw == 16 ? 0 : (lpw == 32 ? 1 : 2)];
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, n_steps, n_envs, rewards, values,
+                     episode_starts, last_values, dones, g, gl, advantages, returns);
   HIPCHK(hipGetLastError());
   return 0;
 }

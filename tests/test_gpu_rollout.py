@@ -28,9 +28,9 @@ def numpy_gae(rewards, values, episode_starts, last_values, dones, gamma, gae_la
 
 @pytest.mark.parametrize("T,N", [(257, 1000), (2048, 32768), (37, 65541), (15, 70)])
 def test_gae_bitexact(gpu, T, N):
-    """The pipelined GAE kernel (16-step blocks, a ragged top block first) at cfg4's per-GPU share
-    2 048 x 32 768 (half-populated waves), a ragged 65 541 envs (full waves) and short rollouts
-    (no whole block), bit for bit against buffers.py:403-438's numpy float32 recurrence."""
+    """The pipelined GAE kernel (32-step load blocks, a ragged top block first, full waves) at
+    cfg4's per-GPU share 2 048 x 32 768, a ragged 65 541 envs and short rollouts (no whole block),
+    bit for bit against buffers.py:403-438's numpy float32 recurrence."""
     import torch
     from f16_jsb_amd.rollout import DeviceRolloutBuffer
     rng = np.random.default_rng(T)
