@@ -22,6 +22,8 @@ import torch
 from .abi import F16_FLAG_NO_AUTORESET, F16_OBS_DIM, F16_SLOT_CLIP, RolloutSlot
 
 FIELDS = ("frames", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns")
+# device memory the deferred timeout bootstrap may take for its stash of terminal observations
+STASH_MAX_BYTES = 1 << 30
 
 
 class DeviceRolloutBuffer:
@@ -184,10 +186,12 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
             and not (int(getattr(envs, "cfg").flags) & F16_FLAG_NO_AUTORESET)
         if bootstrap not in ("deferred", "per_step"):
             raise ValueError("bootstrap must be 'deferred' or 'per_step'")
+        # a lane truncates at most once per max_steps steps (auto-reset restarts its counter),
+        # so it enters the stash at most (T - 1) // max_steps + 1 times in T steps; a stash that
+        # would pass STASH_MAX_BYTES (very short TimeLimits) falls back to the per-step bootstrap
+        cap = n * ((T - 1) // max(1, int(envs.cfg.max_steps)) + 1)
+        defer = defer and cap * buf.k * F16_OBS_DIM * 4 <= STASH_MAX_BYTES
         if defer:
-            # a lane truncates at most once per max_steps steps (auto-reset restarts its counter),
-            # so it enters the stash at most (T - 1) // max_steps + 1 times in T steps
-            cap = n * ((T - 1) // max(1, int(envs.cfg.max_steps)) + 1)
             stash = torch.empty((cap, buf.k, F16_OBS_DIM), dtype=torch.float32, device=dev)
             stash_idx = torch.empty(cap, dtype=torch.int64, device=dev)
             stash_n = torch.zeros(1, dtype=torch.int32, device=dev)
