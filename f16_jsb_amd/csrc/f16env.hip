@@ -1868,23 +1868,57 @@ __device__ __forceinline__ void quat_mul_ref(const float* a, const float* b, flo
   o[2] = a[0] * b[2] + b[0] * a[2] + cy;
   o[3] = a[0] * b[3] + b[0] * a[3] + cz;
 }
-__global__ void f16_poses_kernel(int64_t n, const float* __restrict__ frames, int64_t stride, float* __restrict__ out) {
+// 256 envs per block; 16-B aligned frames (the windowed layout's 64-B slots) are read as
+// 3 x float4 + float2 + float, and the block's 256 x 10 poses leave through LDS as contiguous
+// float4 (a 40-B row per lane would be 10 partial-line dword stores)
+__global__ __launch_bounds__(256) void f16_poses_kernel(int64_t n, const float* __restrict__ frames, int64_t stride,
+                                                        float* __restrict__ out) {
 #pragma clang fp contract(off)
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const float* f = frames + k * stride;
-  const float s = 1e-3f;
-  float* o = out + k * 10;
-  o[0] = -f[1] * s; o[1] = f[2] * s; o[2] = f[0] * s;
-  const float hp = f[9] / 2.0f, ht = f[10] / 2.0f, hs = f[11] / 2.0f;
-  const float q1[4] = {cosf(hp), sinf(hp), 0.0f, 0.0f};
-  const float q2[4] = {cosf(ht), 0.0f, sinf(ht), 0.0f};
-  const float q3[4] = {cosf(hs), 0.0f, 0.0f, sinf(hs)};
-  float q32[4], q[4];
-  quat_mul_ref(q3, q2, q32);
-  quat_mul_ref(q32, q1, q);
-  o[3] = q[0]; o[4] = -q[2]; o[5] = -q[3]; o[6] = q[1];
-  o[7] = -f[13] * s; o[8] = f[14] * s; o[9] = f[12] * s;
+  __shared__ __align__(16) float sOut[256 * 10];
+  const int t = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * 256, k = k0 + t;
+  const int nb = (int)(n - k0 < 256 ? n - k0 : 256);
+  if (t < nb) {
+    const float* f = frames + k * stride;
+    float x[F16_OBS_DIM];
+    if ((stride & 3) == 0 && ((uintptr_t)frames & 15) == 0) {
+      const float4* q4 = reinterpret_cast<const float4*>(f);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 v = q4[j];
+        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+      }
+      const float2 v2 = *reinterpret_cast<const float2*>(f + 12);
+      x[12] = v2.x; x[13] = v2.y; x[14] = f[14];
+    } else {
+#pragma unroll
+      for (int j = 0; j < F16_OBS_DIM; ++j) x[j] = f[j];
+    }
+    const float s = 1e-3f;
+    float* o = sOut + t * 10;
+    o[0] = -x[1] * s; o[1] = x[2] * s; o[2] = x[0] * s;
+    const float hp = x[9] / 2.0f, ht = x[10] / 2.0f, hs = x[11] / 2.0f;
+    float sp, cp, st, ct, ss, cs;
+    sincosf(hp, &sp, &cp);
+    sincosf(ht, &st, &ct);
+    sincosf(hs, &ss, &cs);
+    const float q1[4] = {cp, sp, 0.0f, 0.0f};
+    const float q2[4] = {ct, 0.0f, st, 0.0f};
+    const float q3[4] = {cs, 0.0f, 0.0f, ss};
+    float q32[4], q[4];
+    quat_mul_ref(q3, q2, q32);
+    quat_mul_ref(q32, q1, q);
+    o[3] = q[0]; o[4] = -q[2]; o[5] = -q[3]; o[6] = q[1];
+    o[7] = -x[13] * s; o[8] = x[14] * s; o[9] = x[12] * s;
+  }
+  __syncthreads();
+  float* g = out + k0 * 10;
+  if (nb == 256 && ((uintptr_t)g & 15) == 0) {
+    for (int q = t; q < 256 * 10 / 4; q += 256)
+      reinterpret_cast<float4*>(g)[q] = reinterpret_cast<const float4*>(sOut)[q];
+  } else {
+    for (int q = t; q < nb * 10; q += 256) g[q] = sOut[q];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
