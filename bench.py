@@ -522,28 +522,52 @@ def features_bench(envs, stream, iters=200):
     def stepf(use):
         if envs.window:
             o = envs.step(act).obs
-            if use:
+            if use == 1:
                 features(o, out)
+            elif use == 2:  # the feature window: one frame per env transformed per step
+                envs.obs_features()
         else:
             envs.step(act, features=out if use else None)
 
-    for _ in range(5):
-        stepf(True)
-    t = []
-    for use in (False, True, False, True):
-        s.record(stream)
-        for _ in range(iters // 2):
+    modes = (0, 1, 2) if envs.window else (0, 1)
+    for use in modes:
+        for _ in range(5):
             stepf(use)
-        e.record(stream)
-        torch.cuda.synchronize()
-        t.append(s.elapsed_time(e) / (iters // 2))
-    plain, fused = min(t[0], t[2]), min(t[1], t[3])
+    t = {m: [] for m in modes}
+    for _ in range(2):
+        for use in modes:
+            s.record(stream)
+            for _ in range(iters // 2):
+                stepf(use)
+            e.record(stream)
+            torch.cuda.synchronize()
+            t[use].append(s.elapsed_time(e) / (iters // 2))
+    plain, fused = min(t[0]), min(t[1])
+    fw = {}
+    if envs.window:
+        # the feature-window kernel alone: graph replay of the incremental call after a step
+        # (the step and the call are captured together; the step's own replay is subtracted)
+        def one_step():
+            envs.step(act)
+
+        def step_and_window():
+            envs.step(act)
+            envs.obs_features()
+
+        g_step = graph_ms(one_step, iters // 4)
+        g_both = graph_ms(step_and_window, iters // 4)
+        fw = {"step_with_feature_window_ms": round(min(t[2]), 5),
+              "feature_window_kernel": "f16_feature_window_kernel",
+              "feature_window_bytes_per_env": 64 + 2 * 68,
+              "feature_window_calls": dict(envs.feature_window_calls)}
+        if g_step is not None and g_both is not None:
+            fw["feature_window_ms_graph"] = round(g_both - g_step, 5)
     return {"kernel": "f16_features_strided_kernel" if envs.window else "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
             "timing": "HIP-graph replay of %d launches (kernel + launch boundary)" % iters if gms is not None
             else "host-driven launches", "host_driven_ms": round(host_ms, 5),
             "frames_per_s": round(frames / (ms * 1e-3), 1), "achieved_GBps": round(gbps, 1),
             "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128,
-            "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5)}
+            "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5), **fw}
 
 
 def telemetry_bench(envs, stream, iters=200):

@@ -59,6 +59,7 @@ def lib():
     _set(L, "f16env_step_window_waves_per_simd", [vp], i32)
     _set(L, "f16env_step_mode", [vp], i32)
     _set(L, "f16env_features_strided", [vp, i64, i32, vp, i64, i64, vp], i32)
+    _set(L, "f16env_features_window_step", [vp, i64, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, vp, i32], i32)
     _set(L, "f16env_set_window_order", [vp, i32], i32)
     _set(L, "f16env_window_clear_fresh", [vp, vp], i32)
     _set(L, "f16env_window_bind", [vp, vp, vp, i64, vp, vp, vp, vp, vp], i32)
@@ -120,7 +121,7 @@ EXPORTED_SYMBOLS = (
     "f16env_config_default", "f16env_config_cfg5", "f16env_create", "f16env_destroy", "f16env_state_bytes",
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_obs_bounds_count", "f16env_debug_checks", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
-    "f16env_step_mode", "f16env_features_strided", "f16env_set_window_order", "f16env_window_clear_fresh",
+    "f16env_step_mode", "f16env_features_strided", "f16env_features_window_step", "f16env_set_window_order", "f16env_window_clear_fresh",
     "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt", "f16env_window_step_rollout",
     "f16env_window_rollout_random", "f16env_bootstrap_timeouts", "f16env_bootstrap_stash", "f16env_bootstrap_apply", "f16env_abi_version",
     "f16env_get_state",

@@ -1852,6 +1852,97 @@ __global__ __launch_bounds__(256) void f16_features_strided_kernel(int64_t n_row
   }
 }
 
+// Feature window (windowed layout): the policy features of both frame histories kept beside
+// them, position-major [T][N][17], so that after a windowed step only the frame the step wrote
+// needs transforming -- the features of a K-frame observation cost one frame per step instead
+// of K (f16env_features_strided over the view). The step wrote position p of both histories:
+// wx[p] = the new frame (or the reset frame of a lane reset by the step), wy[p] = the new frame.
+// Mirrored here: fx[p] = feat(wx[p]); fy[p] = feat(wy[p]) (the same as fx[p] unless the lane was
+// reset, then read); and the step's window fills of reset lanes -- a lane reset BY this step
+// fills wx[p-K+1 .. p-1] with its reset frame (= fx[p]); a lane reset by the previous step
+// (FRESH: prev_done) fills them from wy[p-1] (= fy[p-1]), the reset one winning when both hold.
+// prev_done records this step's resets for the next call. One lane per env; the block's fx[p]
+// and fy[p] rows leave through LDS as coalesced float4 (they are 256 * 17 contiguous floats).
+struct FeatWinArgs {
+  const float* wx;
+  const float* wy;
+  int64_t wrow, wenv;  // frame-history strides (floats) between positions, between envs
+  float* fx;
+  float* fy;           // [T][N][17]
+  int64_t n;
+  int32_t K, p, autoreset;
+  const uint8_t* term;
+  const uint8_t* trunc;
+  uint8_t* prev_done;
+};
+__global__ __launch_bounds__(256) void f16_feature_window_kernel(FeatWinArgs a) {
+  __shared__ __align__(16) float sX[256 * FEAT_OUT];
+  __shared__ __align__(16) float sY[256 * FEAT_OUT];
+  const int t = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * 256, k = k0 + t;
+  const int nb = (int)(a.n - k0 < 256 ? a.n - k0 : 256);
+  const int64_t rowN = a.n * FEAT_OUT;  // floats between feature positions
+  bool done = false, fresh = false;
+  if (t < nb) {
+    F16_CHECK(k < a.n && a.p >= a.K - 1, DBG_FRAME_INDEX);
+    const float4* q = reinterpret_cast<const float4*>(a.wx + k * a.wenv + (int64_t)a.p * a.wrow);
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 v = q[j];
+      x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+    }
+    done = a.autoreset && (a.term[k] | a.trunc[k]) != 0;
+    fresh = a.prev_done[k] != 0;
+    frame_features(x, sX + t * FEAT_OUT);
+    if (done) {  // reset by this step: wy[p] holds the final frame, wx[p] the reset frame
+      const float4* qy = reinterpret_cast<const float4*>(a.wy + k * a.wenv + (int64_t)a.p * a.wrow);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = qy[j];
+        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+      }
+      frame_features(x, sY + t * FEAT_OUT);
+    } else {
+#pragma unroll
+      for (int j = 0; j < FEAT_OUT; ++j) sY[t * FEAT_OUT + j] = sX[t * FEAT_OUT + j];
+    }
+    a.prev_done[k] = done ? 1 : 0;
+  }
+  // the window fills (rare: lanes reset by this or the previous step); positions below p only,
+  // so they never meet the block's row-p stores below
+  if (t < nb && a.K > 1 && (done || fresh)) {
+    float y[FEAT_OUT];
+    if (done) {
+#pragma unroll
+      for (int j = 0; j < FEAT_OUT; ++j) y[j] = sX[t * FEAT_OUT + j];
+    } else {
+      const float* src = a.fy + (int64_t)(a.p - 1) * rowN + k * FEAT_OUT;
+#pragma unroll
+      for (int j = 0; j < FEAT_OUT; ++j) y[j] = src[j];
+    }
+    for (int r = a.p - a.K + 1; r < a.p; ++r) {
+      float* d = a.fx + (int64_t)r * rowN + k * FEAT_OUT;
+#pragma unroll
+      for (int j = 0; j < FEAT_OUT; ++j) d[j] = y[j];
+    }
+  }
+  __syncthreads();
+  float* gx = a.fx + (int64_t)a.p * rowN + k0 * FEAT_OUT;
+  float* gy = a.fy + (int64_t)a.p * rowN + k0 * FEAT_OUT;
+  if (nb == 256 && ((((uintptr_t)gx) | ((uintptr_t)gy)) & 15) == 0) {
+    for (int q = t; q < 256 * FEAT_OUT / 4; q += 256) {
+      reinterpret_cast<float4*>(gx)[q] = reinterpret_cast<const float4*>(sX)[q];
+      reinterpret_cast<float4*>(gy)[q] = reinterpret_cast<const float4*>(sY)[q];
+    }
+  } else {
+    for (int q = t; q < nb * FEAT_OUT; q += 256) {
+      gx[q] = sX[q];
+      gy[q] = sY[q];
+    }
+  }
+}
+
 // Render/telemetry poses of one frame per env: what JSBSimEnv.render
 // (jsbsim_gym/jsbsim_gym.py:381-415) hands the Viewer -- the aircraft position in viewer axes
 // (-y, h, x) * 1e-3, its attitude Quaternion.from_euler(phi, theta, psi) (visualization/
@@ -2882,6 +2973,29 @@ int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float
   if (blocks > 0x7fffffffLL) return set_err(-1, "too many frames");
   hipLaunchKernelGGL(f16_features_strided_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_rows, K,
                      obs, row_stride, frame_stride, feat);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_features_window_step(void* stream, int64_t n, int32_t K, int32_t pos, const float* hist_cur,
+                                const float* hist_other, int64_t pos_stride, int64_t env_stride, float* feat_cur,
+                                float* feat_other, const uint8_t* terminated, const uint8_t* truncated,
+                                uint8_t* prev_done, int32_t autoreset) {
+  if (n < 0 || K < 1 || pos < K - 1) return set_err(-1, "n >= 0, K >= 1 and pos >= K - 1 required");
+  if (n == 0) return 0;
+  if (!hist_cur || !hist_other || !feat_cur || !feat_other || !terminated || !truncated || !prev_done)
+    return set_err(-1, "null argument");
+  if ((pos_stride & 15) || (env_stride & 15) || pos_stride < 16 || env_stride < 16 ||
+      ((((uintptr_t)hist_cur) | ((uintptr_t)hist_other)) & 15) != 0)
+    return set_err(-1, "frame histories must be 16-byte aligned with 16-float slots");
+  if (((((uintptr_t)feat_cur) | ((uintptr_t)feat_other)) & 3) != 0) return set_err(-1, "feature histories must be float-aligned");
+  FeatWinArgs a;
+  a.wx = hist_cur; a.wy = hist_other; a.wrow = pos_stride; a.wenv = env_stride;
+  a.fx = feat_cur; a.fy = feat_other; a.n = n; a.K = K; a.p = pos; a.autoreset = autoreset ? 1 : 0;
+  a.term = terminated; a.trunc = truncated; a.prev_done = prev_done;
+  const int64_t blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffLL) return set_err(-1, "too many envs");
+  hipLaunchKernelGGL(f16_feature_window_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   HIPCHK(hipGetLastError());
   return 0;
 }

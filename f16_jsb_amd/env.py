@@ -112,6 +112,14 @@ class F16Envs:
             self._views = [[None] * T for _ in range(2)]
             self._p = k - 1   # newest frame position of the current observation's window
             self._obs = None
+            # feature window (obs_features): feature histories beside the frame histories, made
+            # at the first call; op counters tell whether they describe the current windows
+            self._fh = None
+            self._op = 0          # ops that changed the windows (steps, resets, state / obs writes)
+            self._step_op = -1    # the last op that was a step
+            self._feat_op = -1    # the op the feature windows describe
+            self._feat_prev_ok = False  # prev_done holds the last step's resets
+            self.feature_window_calls = {"incremental": 0, "full": 0}
         else:
             self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
         self._cur = 0
@@ -222,6 +230,7 @@ class F16Envs:
         if self.window:
             check(lib().f16env_reset_window(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c),
                                             self._hist_ptr[self._cur], self.T, self._p), "f16env_reset_window")
+            self._op += 1
             return self._window()
         out = self._obs[self._cur]
         check(lib().f16env_reset(self._h, self._stream(), _ptr(m), _ptr(g), _ptr(c), _ptr(out)), "f16env_reset")
@@ -311,11 +320,16 @@ class F16Envs:
         if p >= self.T:  # move the last K-1 frames to the front of both histories
             check(lib().f16env_window_restart(self._h, s, self._hist_ptr[0], self._hist_ptr[1], self.T, self._p),
                   "f16env_window_restart")
+            if self._fh is not None and self._feat_op == self._op:  # the feature windows move along
+                k = self.k
+                self._fh[:, :k - 1].copy_(self._fh[:, self._p - k + 2:self._p + 1])
             p = self.k - 1
         return s, self._cur ^ 1, p
 
     def _advanced(self, cur, p) -> StepOut:
         self._cur, self._p = cur, p
+        self._op += 1
+        self._step_op = self._op
         self.terminal_obs = self._window(1)
         return StepOut(self._window(), self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return,
                        self.ep_len)
@@ -418,6 +432,7 @@ class F16Envs:
                                                      _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(last_start)),
                   "f16env_window_rollout_random")
             self._p = q
+            self._op += 1
             self.terminal_obs = self._window(1)
             return
         prev = self._obs[self._cur]
@@ -472,6 +487,8 @@ class F16Envs:
         if tuple(s.shape) != (self.n, F16C_N):
             raise ValueError("state must be (N, %d)" % F16C_N)
         check(lib().f16env_set_state(self._h, self._stream(), _ptr(s)), "f16env_set_state")
+        if self.window:
+            self._op += 1
         self.torch.cuda.current_stream(self.device).synchronize()
 
     def set_obs(self, obs):
@@ -483,8 +500,61 @@ class F16Envs:
             self._window(1).copy_(o)
             # both windows are whole now: lanes reset before this need no refill at the next step
             check(lib().f16env_window_clear_fresh(self._h, self._stream()), "f16env_window_clear_fresh")
+            self._op += 1
         else:
             self._obs[self._cur].copy_(o)
+
+    def obs_features(self):
+        """(N, K, 17) float32 policy features of the current observation (features.py:37-67 per
+        frame; LMA_features.py:757-765 over the stack), equal bit for bit to
+        features.features(self.obs). Windowed layout: kept in two feature histories beside the
+        frame histories ([T][N][17] per parity, position-major; the result is a view, valid
+        until the next step as self.obs), so a call after each step transforms one frame per
+        env (f16env_features_window_step) instead of K. The first call, and a call after a
+        reset, set_state, set_obs, rollout_random or after a step not followed by a call,
+        transforms both whole windows; so does the first call after that when it was not a
+        step. Contiguous layout: features(self.obs)."""
+        from .features import FEATURES_DIM, features
+        if not self.window:
+            return features(self.obs)
+        t = self.torch
+        n, k, L = self.n, self.k, lib()
+        if self._fh is None:
+            self._fh = t.zeros((2, self.T, n, FEATURES_DIM), dtype=t.float32, device=self.device)
+            self._fh_ptr = (self._fh[0].data_ptr(), self._fh[1].data_ptr())
+            self._prev_done = t.zeros(n, dtype=t.uint8, device=self.device)
+            self._fviews = [[None] * self.T for _ in range(2)]
+        cur, p = self._cur, self._p
+        if self._feat_op != self._op:
+            wrow, wenv = (16, self.T * 16) if self._env_major else (n * 16, 16)
+            autoreset = 0 if int(self.cfg.flags) & F16_FLAG_NO_AUTORESET else 1
+            s = self._stream()
+            if self._feat_prev_ok and self._feat_op == self._op - 1 and self._step_op == self._op:
+                check(L.f16env_features_window_step(s, n, k, p, self._hist_ptr[cur], self._hist_ptr[cur ^ 1], wrow, wenv,
+                                                    self._fh_ptr[cur], self._fh_ptr[cur ^ 1], self.term.data_ptr(),
+                                                    self.trunc.data_ptr(), self._prev_done.data_ptr(), autoreset),
+                      "f16env_features_window_step")
+                self.feature_window_calls["incremental"] += 1
+            else:
+                self.feature_window_calls["full"] += 1
+                for b in (cur, cur ^ 1):  # positions p-K+1 .. p of history b: K "rows" of N frames
+                    check(L.f16env_features_strided(s, k, n, self._hist[b].data_ptr() + 4 * (p - k + 1) * wrow, wrow,
+                                                    wenv, self._fh_ptr[b] + 4 * (p - k + 1) * n * FEATURES_DIM),
+                          "f16env_features_strided")
+                # the next step's window fills mirror the resets of the step that made this state
+                # (FRESH lanes); after any other op they are unknown here, so that step's call
+                # transforms whole windows again
+                self._feat_prev_ok = self._step_op == self._op
+                if self._feat_prev_ok:
+                    if autoreset:
+                        self._prev_done.copy_((self.term | self.trunc) != 0)
+                    else:
+                        self._prev_done.zero_()
+            self._feat_op = self._op
+        v = self._fviews[cur][p]
+        if v is None:
+            v = self._fviews[cur][p] = self._fh[cur, p - k + 1:p + 1].transpose(0, 1)
+        return v
 
     def trim(self, ic):
         t = self.torch

@@ -421,6 +421,21 @@ int f16env_features(void* stream, int64_t n_frames, const float* obs, float* fea
 int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float* obs, int64_t row_stride,
                             int64_t frame_stride, float* feat);
 
+/* Feature window (ABI 3, windowed layout): keeps the features of both frame histories in two
+ * position-major feature histories feat_cur / feat_other ([T][N][17] float32, parity as the
+ * frame histories) after a windowed step that wrote position `pos`, transforming only that
+ * position's frames plus the window fills of the lanes reset by this step or the previous one
+ * (prev_done: N bytes, the previous call's resets in, this step's out; autoreset 0 = the handle
+ * runs with F16_FLAG_NO_AUTORESET). Precondition: both feature windows [pos-K .. pos-1] hold
+ * the features of the frame windows before the step, prev_done the resets of that step (a
+ * fresh start: f16env_features_strided over both windows, prev_done from the last step's
+ * flags). Replaces the per-step f16env_features_strided over the whole (N, K, 15) view
+ * (features.py:37-67 per frame, LMA_features.py:757-765 over the stack). */
+int f16env_features_window_step(void* stream, int64_t n, int32_t K, int32_t pos, const float* hist_cur,
+                                const float* hist_other, int64_t pos_stride, int64_t env_stride, float* feat_cur,
+                                float* feat_other, const uint8_t* terminated, const uint8_t* truncated,
+                                uint8_t* prev_done, int32_t autoreset);
+
 /* Render/telemetry poses, replacing the state -> Viewer transform of
  * jsbsim_gym.py:381-415 (JSBSimEnv.render) for every env at once, float32:
  *   frames  n frames of 15 floats, frame i at frames + i * frame_stride (e.g. the newest frame
