@@ -59,7 +59,7 @@ def lib():
     _set(L, "f16env_step_window_waves_per_simd", [vp], i32)
     _set(L, "f16env_step_mode", [vp], i32)
     _set(L, "f16env_features_strided", [vp, i64, i32, vp, i64, i64, vp], i32)
-    _set(L, "f16env_features_window_step", [vp, i64, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, vp, i32], i32)
+    _set(L, "f16env_features_window_step", [vp, i64, i32, i32, vp, i64, i64, vp, vp, vp, vp, i32, i32], i32)
     _set(L, "f16env_set_window_order", [vp, i32], i32)
     _set(L, "f16env_window_clear_fresh", [vp, vp], i32)
     _set(L, "f16env_window_bind", [vp, vp, vp, i64, vp, vp, vp, vp, vp], i32)

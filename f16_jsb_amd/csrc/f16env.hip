@@ -160,6 +160,34 @@ __device__ __forceinline__ void frame_features(const float* o, float* y) {
   y[15] = cosf(rel_bearing); y[16] = sinf(rel_bearing);                   // :65
 }
 
+// frame_features split into four parts of about equal cost (the feature-window kernel gives
+// each part to a wave): the same expressions, so the same values, as frame_features
+__device__ __forceinline__ void frame_features_part(const float* o, float* y, int part) {
+#pragma clang fp contract(off)
+  const float dx = o[12] - o[0], dy = o[13] - o[1];
+  if (part == 0) {
+    const float abs_bearing = atan2f(dy, dx);
+    const float rel_bearing = abs_bearing - o[11];
+    y[15] = cosf(rel_bearing); y[16] = sinf(rel_bearing);
+  } else if (part == 1) {
+    y[7] = cosf(o[4]); y[8] = cosf(o[5]);
+    y[9] = sinf(o[4]); y[10] = sinf(o[5]);
+  } else if (part == 2) {
+    y[11] = cosf(o[9]); y[12] = cosf(o[10]);
+    y[13] = sinf(o[9]); y[14] = sinf(o[10]);
+  } else {
+    const float dz = o[14] - o[2];
+    float d2 = dx * dx;
+    d2 = __fadd_rn(d2, __fmul_rn(dy, dy));
+    const float distance = __fsqrt_rn(d2);
+    y[0] = __fdiv_rn(1.0f, __fadd_rn(1.0f, __fmul_rn(distance, 1e-3f)));
+    y[1] = __fdiv_rn(dz, 15000.0f);
+    y[2] = __fdiv_rn(o[2], 15000.0f);
+    y[3] = o[3];
+    y[4] = o[6]; y[5] = o[7]; y[6] = o[8];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
 // ------------------------------------------------------------------------------------------
@@ -1856,88 +1884,86 @@ __global__ __launch_bounds__(256) void f16_features_strided_kernel(int64_t n_row
 // them, position-major [T][N][17], so that after a windowed step only the frame the step wrote
 // needs transforming -- the features of a K-frame observation cost one frame per step instead
 // of K (f16env_features_strided over the view). The step wrote position p of both histories:
-// wx[p] = the new frame (or the reset frame of a lane reset by the step), wy[p] = the new frame.
-// Mirrored here: fx[p] = feat(wx[p]); fy[p] = feat(wy[p]) (the same as fx[p] unless the lane was
-// reset, then read); and the step's window fills of reset lanes -- a lane reset BY this step
-// fills wx[p-K+1 .. p-1] with its reset frame (= fx[p]); a lane reset by the previous step
-// (FRESH: prev_done) fills them from wy[p-1] (= fy[p-1]), the reset one winning when both hold.
-// prev_done records this step's resets for the next call. One lane per env; the block's fx[p]
-// and fy[p] rows leave through LDS as coalesced float4 (they are 256 * 17 contiguous floats).
+// wx[p] = the new frame, or the reset frame of a lane reset by the step (which also fills
+// wx[p-K+1 .. p-1] with it), wy[p] = the new frame (the reset lane's final frame). Here
+// fx[p] = fy[p] = y = feat(wx[p]), and a reset lane writes y over fx[p-K+1 .. p-1] too -- and
+// over fy[p-K+2 .. p]: the window fill the NEXT step will make of that lane (FRESH: wx' = wy
+// gets wx[p] at positions p-K+2 .. p, step_body) applied ahead, so no call needs the previous
+// step's resets or a second transform; fy's window then holds the next step's view, not the
+// terminal observation's (whose features nobody asks for). No dependent load. 64 envs per
+// 256-thread block: the block's 64 frame slots come in as one float4 per thread (coalesced),
+// then each of the 4 waves computes one quarter of every env's 17 features from LDS
+// (frame_features_part: the work per wave a quarter, four waves per SIMD at 65 536 envs instead
+// of one -- the one-lane-per-env form was latency-bound at 6.2 us, gpurun fw r04), and the
+// block's rows p (64 * 17 contiguous floats in each history) leave as float4. transform = 0:
+// only the ahead fills of the step's reset lanes, y read from fx[p] (after both windows were
+// transformed whole following a step).
 struct FeatWinArgs {
   const float* wx;
-  const float* wy;
   int64_t wrow, wenv;  // frame-history strides (floats) between positions, between envs
   float* fx;
   float* fy;           // [T][N][17]
   int64_t n;
-  int32_t K, p, autoreset;
+  int32_t K, p, autoreset, transform;
   const uint8_t* term;
   const uint8_t* trunc;
-  uint8_t* prev_done;
 };
+static constexpr int FW_ENVS = 64;     // envs per block
+static constexpr int FW_IN = 17;       // LDS pitch of a frame (odd: conflict-free per-env reads)
 __global__ __launch_bounds__(256) void f16_feature_window_kernel(FeatWinArgs a) {
-  __shared__ __align__(16) float sX[256 * FEAT_OUT];
-  __shared__ __align__(16) float sY[256 * FEAT_OUT];
-  const int t = threadIdx.x;
-  const int64_t k0 = (int64_t)blockIdx.x * 256, k = k0 + t;
-  const int nb = (int)(a.n - k0 < 256 ? a.n - k0 : 256);
+  __shared__ __align__(16) float sIn[FW_ENVS * FW_IN];
+  __shared__ __align__(16) float sY[FW_ENVS * FEAT_OUT];
+  const int t = threadIdx.x, w = t >> 6, e = t & 63;
+  const int64_t k0 = (int64_t)blockIdx.x * FW_ENVS, k = k0 + e;
+  const int nb = (int)(a.n - k0 < FW_ENVS ? a.n - k0 : FW_ENVS);
   const int64_t rowN = a.n * FEAT_OUT;  // floats between feature positions
-  bool done = false, fresh = false;
-  if (t < nb) {
-    F16_CHECK(k < a.n && a.p >= a.K - 1, DBG_FRAME_INDEX);
-    const float4* q = reinterpret_cast<const float4*>(a.wx + k * a.wenv + (int64_t)a.p * a.wrow);
-    float x[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 v = q[j];
-      x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+  F16_CHECK(nb > 0 && a.p >= a.K - 1, DBG_FRAME_INDEX);
+  const bool done = e < nb && a.autoreset && (a.term[k] | a.trunc[k]) != 0;
+  if (a.transform) {
+    const int le = t >> 2, qq = t & 3;  // the block's slots: thread t loads quarter qq of env le
+    if (le < nb) {
+      const float4 v = *reinterpret_cast<const float4*>(a.wx + (k0 + le) * a.wenv + (int64_t)a.p * a.wrow + 4 * qq);
+      float* d = sIn + le * FW_IN + 4 * qq;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
-    done = a.autoreset && (a.term[k] | a.trunc[k]) != 0;
-    fresh = a.prev_done[k] != 0;
-    frame_features(x, sX + t * FEAT_OUT);
-    if (done) {  // reset by this step: wy[p] holds the final frame, wx[p] the reset frame
-      const float4* qy = reinterpret_cast<const float4*>(a.wy + k * a.wenv + (int64_t)a.p * a.wrow);
+    __syncthreads();
+    if (e < nb) frame_features_part(sIn + e * FW_IN, sY + e * FEAT_OUT, w);
+    __syncthreads();
+  }
+  if (done && a.K > 1) {  // rare: the reset lanes' window fills (rows below p in fx, ahead in fy)
+    // wave w writes features j = w, w+4, ... of env e
+    float v[5];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = qy[j];
-        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+    for (int i = 0; i < 5; ++i) {
+      const int j = w + 4 * i;
+      v[i] = j < FEAT_OUT ? (a.transform ? sY[e * FEAT_OUT + j] : a.fx[(int64_t)a.p * rowN + k * FEAT_OUT + j]) : 0.0f;
+    }
+    for (int r = a.p - a.K + 1; r <= a.p; ++r) {
+      float* dx = a.fx + (int64_t)r * rowN + k * FEAT_OUT;
+      float* dy = a.fy + (int64_t)r * rowN + k * FEAT_OUT;
+      const bool wx_ = r < a.p, wy_ = r > a.p - a.K + 1 && (r < a.p || !a.transform);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int j = w + 4 * i;
+        if (j < FEAT_OUT) {
+          if (wx_) dx[j] = v[i];
+          if (wy_) dy[j] = v[i];
+        }
       }
-      frame_features(x, sY + t * FEAT_OUT);
-    } else {
-#pragma unroll
-      for (int j = 0; j < FEAT_OUT; ++j) sY[t * FEAT_OUT + j] = sX[t * FEAT_OUT + j];
-    }
-    a.prev_done[k] = done ? 1 : 0;
-  }
-  // the window fills (rare: lanes reset by this or the previous step); positions below p only,
-  // so they never meet the block's row-p stores below
-  if (t < nb && a.K > 1 && (done || fresh)) {
-    float y[FEAT_OUT];
-    if (done) {
-#pragma unroll
-      for (int j = 0; j < FEAT_OUT; ++j) y[j] = sX[t * FEAT_OUT + j];
-    } else {
-      const float* src = a.fy + (int64_t)(a.p - 1) * rowN + k * FEAT_OUT;
-#pragma unroll
-      for (int j = 0; j < FEAT_OUT; ++j) y[j] = src[j];
-    }
-    for (int r = a.p - a.K + 1; r < a.p; ++r) {
-      float* d = a.fx + (int64_t)r * rowN + k * FEAT_OUT;
-#pragma unroll
-      for (int j = 0; j < FEAT_OUT; ++j) d[j] = y[j];
     }
   }
-  __syncthreads();
+  if (!a.transform) return;
   float* gx = a.fx + (int64_t)a.p * rowN + k0 * FEAT_OUT;
   float* gy = a.fy + (int64_t)a.p * rowN + k0 * FEAT_OUT;
-  if (nb == 256 && ((((uintptr_t)gx) | ((uintptr_t)gy)) & 15) == 0) {
-    for (int q = t; q < 256 * FEAT_OUT / 4; q += 256) {
-      reinterpret_cast<float4*>(gx)[q] = reinterpret_cast<const float4*>(sX)[q];
-      reinterpret_cast<float4*>(gy)[q] = reinterpret_cast<const float4*>(sY)[q];
+  if (nb == FW_ENVS && ((((uintptr_t)gx) | ((uintptr_t)gy)) & 15) == 0) {
+    for (int q = t; q < FW_ENVS * FEAT_OUT / 4; q += 256) {
+      const float4 v = reinterpret_cast<const float4*>(sY)[q];
+      reinterpret_cast<float4*>(gx)[q] = v;
+      reinterpret_cast<float4*>(gy)[q] = v;
     }
   } else {
     for (int q = t; q < nb * FEAT_OUT; q += 256) {
-      gx[q] = sX[q];
+      gx[q] = sY[q];
       gy[q] = sY[q];
     }
   }
@@ -2978,22 +3004,21 @@ int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float
 }
 
 int f16env_features_window_step(void* stream, int64_t n, int32_t K, int32_t pos, const float* hist_cur,
-                                const float* hist_other, int64_t pos_stride, int64_t env_stride, float* feat_cur,
-                                float* feat_other, const uint8_t* terminated, const uint8_t* truncated,
-                                uint8_t* prev_done, int32_t autoreset) {
+                                int64_t pos_stride, int64_t env_stride, float* feat_cur, float* feat_other,
+                                const uint8_t* terminated, const uint8_t* truncated, int32_t autoreset,
+                                int32_t transform) {
   if (n < 0 || K < 1 || pos < K - 1) return set_err(-1, "n >= 0, K >= 1 and pos >= K - 1 required");
   if (n == 0) return 0;
-  if (!hist_cur || !hist_other || !feat_cur || !feat_other || !terminated || !truncated || !prev_done)
-    return set_err(-1, "null argument");
-  if ((pos_stride & 15) || (env_stride & 15) || pos_stride < 16 || env_stride < 16 ||
-      ((((uintptr_t)hist_cur) | ((uintptr_t)hist_other)) & 15) != 0)
-    return set_err(-1, "frame histories must be 16-byte aligned with 16-float slots");
+  if (!hist_cur || !feat_cur || !feat_other || !terminated || !truncated) return set_err(-1, "null argument");
+  if ((pos_stride & 15) || (env_stride & 15) || pos_stride < 16 || env_stride < 16 || (((uintptr_t)hist_cur) & 15) != 0)
+    return set_err(-1, "frame history must be 16-byte aligned with 16-float slots");
   if (((((uintptr_t)feat_cur) | ((uintptr_t)feat_other)) & 3) != 0) return set_err(-1, "feature histories must be float-aligned");
   FeatWinArgs a;
-  a.wx = hist_cur; a.wy = hist_other; a.wrow = pos_stride; a.wenv = env_stride;
-  a.fx = feat_cur; a.fy = feat_other; a.n = n; a.K = K; a.p = pos; a.autoreset = autoreset ? 1 : 0;
-  a.term = terminated; a.trunc = truncated; a.prev_done = prev_done;
-  const int64_t blocks = (n + 255) / 256;
+  a.wx = hist_cur; a.wrow = pos_stride; a.wenv = env_stride;
+  a.fx = feat_cur; a.fy = feat_other; a.n = n; a.K = K; a.p = pos;
+  a.autoreset = autoreset ? 1 : 0; a.transform = transform ? 1 : 0;
+  a.term = terminated; a.trunc = truncated;
+  const int64_t blocks = (n + FW_ENVS - 1) / FW_ENVS;
   if (blocks > 0x7fffffffLL) return set_err(-1, "too many envs");
   hipLaunchKernelGGL(f16_feature_window_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   HIPCHK(hipGetLastError());

@@ -118,7 +118,7 @@ class F16Envs:
             self._op = 0          # ops that changed the windows (steps, resets, state / obs writes)
             self._step_op = -1    # the last op that was a step
             self._feat_op = -1    # the op the feature windows describe
-            self._feat_prev_ok = False  # prev_done holds the last step's resets
+            self._feat_prev_ok = False  # the feature windows hold the last step's ahead fills
             self.feature_window_calls = {"incremental": 0, "full": 0}
         else:
             self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
@@ -321,8 +321,9 @@ class F16Envs:
             check(lib().f16env_window_restart(self._h, s, self._hist_ptr[0], self._hist_ptr[1], self.T, self._p),
                   "f16env_window_restart")
             if self._fh is not None and self._feat_op == self._op:  # the feature windows move along
-                k = self.k
-                self._fh[:, :k - 1].copy_(self._fh[:, self._p - k + 2:self._p + 1])
+                k = self.k   # (K-1 whole rows: one contiguous device-to-device copy per parity)
+                for b in (0, 1):
+                    self._fh[b, :k - 1].copy_(self._fh[b, self._p - k + 2:self._p + 1])
             p = self.k - 1
         return s, self._cur ^ 1, p
 
@@ -510,46 +511,47 @@ class F16Envs:
         features.features(self.obs). Windowed layout: kept in two feature histories beside the
         frame histories ([T][N][17] per parity, position-major; the result is a view, valid
         until the next step as self.obs), so a call after each step transforms one frame per
-        env (f16env_features_window_step) instead of K. The first call, and a call after a
-        reset, set_state, set_obs, rollout_random or after a step not followed by a call,
-        transforms both whole windows; so does the first call after that when it was not a
-        step. Contiguous layout: features(self.obs)."""
+        env (f16env_features_window_step) instead of K. The first call, a call after a reset,
+        set_state, set_obs or rollout_random, the call after the step that follows one of
+        those, and a call after a step not followed by a call transform both whole windows.
+        Contiguous layout: features(self.obs)."""
         from .features import FEATURES_DIM, features
         if not self.window:
             return features(self.obs)
         t = self.torch
         n, k, L = self.n, self.k, lib()
         if self._fh is None:
-            self._fh = t.zeros((2, self.T, n, FEATURES_DIM), dtype=t.float32, device=self.device)
+            # (positions outside the window are written before they are read)
+            self._fh = t.empty((2, self.T, n, FEATURES_DIM), dtype=t.float32, device=self.device)
             self._fh_ptr = (self._fh[0].data_ptr(), self._fh[1].data_ptr())
-            self._prev_done = t.zeros(n, dtype=t.uint8, device=self.device)
             self._fviews = [[None] * self.T for _ in range(2)]
         cur, p = self._cur, self._p
         if self._feat_op != self._op:
             wrow, wenv = (16, self.T * 16) if self._env_major else (n * 16, 16)
             autoreset = 0 if int(self.cfg.flags) & F16_FLAG_NO_AUTORESET else 1
             s = self._stream()
-            if self._feat_prev_ok and self._feat_op == self._op - 1 and self._step_op == self._op:
-                check(L.f16env_features_window_step(s, n, k, p, self._hist_ptr[cur], self._hist_ptr[cur ^ 1], wrow, wenv,
-                                                    self._fh_ptr[cur], self._fh_ptr[cur ^ 1], self.term.data_ptr(),
-                                                    self.trunc.data_ptr(), self._prev_done.data_ptr(), autoreset),
+            after_step = self._step_op == self._op
+            hc, fc, fo = self._hist_ptr[cur], self._fh_ptr[cur], self._fh_ptr[cur ^ 1]
+            if self._feat_prev_ok and self._feat_op == self._op - 1 and after_step:
+                check(L.f16env_features_window_step(s, n, k, p, hc, wrow, wenv, fc, fo, self.term.data_ptr(),
+                                                    self.trunc.data_ptr(), autoreset, 1),
                       "f16env_features_window_step")
                 self.feature_window_calls["incremental"] += 1
             else:
                 self.feature_window_calls["full"] += 1
                 for b in (cur, cur ^ 1):  # positions p-K+1 .. p of history b: K "rows" of N frames
-                    check(L.f16env_features_strided(s, k, n, self._hist[b].data_ptr() + 4 * (p - k + 1) * wrow, wrow,
-                                                    wenv, self._fh_ptr[b] + 4 * (p - k + 1) * n * FEATURES_DIM),
+                    check(L.f16env_features_strided(s, k, n, self._hist_ptr[b] + 4 * (p - k + 1) * wrow, wrow, wenv,
+                                                    self._fh_ptr[b] + 4 * (p - k + 1) * n * FEATURES_DIM),
                           "f16env_features_strided")
-                # the next step's window fills mirror the resets of the step that made this state
-                # (FRESH lanes); after any other op they are unknown here, so that step's call
-                # transforms whole windows again
-                self._feat_prev_ok = self._step_op == self._op
-                if self._feat_prev_ok:
-                    if autoreset:
-                        self._prev_done.copy_((self.term | self.trunc) != 0)
-                    else:
-                        self._prev_done.zero_()
+                # the next step's window fills of the lanes this state's step reset, applied ahead
+                # (f16env_features_window_step's invariant); after any other op the lanes due a
+                # fill are not known here, so the call after the next step transforms whole
+                # windows again
+                self._feat_prev_ok = after_step
+                if after_step:
+                    check(L.f16env_features_window_step(s, n, k, p, hc, wrow, wenv, fc, fo, self.term.data_ptr(),
+                                                        self.trunc.data_ptr(), autoreset, 0),
+                          "f16env_features_window_step")
             self._feat_op = self._op
         v = self._fviews[cur][p]
         if v is None:

@@ -31,6 +31,7 @@
  *                      rollout (one value evaluation over the stashed terminal observations)
  *   f16env_gae      <- stable_baselines3/common/buffers.py:403-438 (device rollout, 8f rank 1)
  *   f16env_features <- jsbsim_gym/features.py:37-67 JSBSimFeatureExtractor.forward (8f rank 3)
+ *   f16env_features_window_step <- the same per step on a windowed observation, one frame each
  *   f16env_poses    <- jsbsim_gym.py:381-415 JSBSimEnv.render state -> Viewer poses (8f rank 4)
  */
 #ifndef F16ENV_H
@@ -47,7 +48,7 @@ extern "C" {
  * windowed layout's FRESH mark; the rollout slot gained next_frame / flags (F16_SLOT_CLIP);
  * f16env_rollout_random has no stack_k / mode limits; new f16env_window_step_rollout,
  * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_bootstrap_stash,
- * f16env_bootstrap_apply, f16env_abi_version. */
+ * f16env_bootstrap_apply, f16env_features_window_step, f16env_abi_version. */
 #define F16ENV_ABI_VERSION 3
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
@@ -421,20 +422,21 @@ int f16env_features(void* stream, int64_t n_frames, const float* obs, float* fea
 int f16env_features_strided(void* stream, int64_t n_rows, int32_t K, const float* obs, int64_t row_stride,
                             int64_t frame_stride, float* feat);
 
-/* Feature window (ABI 3, windowed layout): keeps the features of both frame histories in two
+/* Feature window (ABI 3, windowed layout): keeps the features of the observation window in two
  * position-major feature histories feat_cur / feat_other ([T][N][17] float32, parity as the
- * frame histories) after a windowed step that wrote position `pos`, transforming only that
- * position's frames plus the window fills of the lanes reset by this step or the previous one
- * (prev_done: N bytes, the previous call's resets in, this step's out; autoreset 0 = the handle
- * runs with F16_FLAG_NO_AUTORESET). Precondition: both feature windows [pos-K .. pos-1] hold
- * the features of the frame windows before the step, prev_done the resets of that step (a
- * fresh start: f16env_features_strided over both windows, prev_done from the last step's
- * flags). Replaces the per-step f16env_features_strided over the whole (N, K, 15) view
- * (features.py:37-67 per frame, LMA_features.py:757-765 over the stack). */
+ * frame histories) after a windowed step that wrote position `pos` of hist_cur (strides in
+ * floats), transforming only that position's frames: feat_cur[pos] = feat_other[pos] =
+ * features of hist_cur[pos]; lanes the step reset (terminated | truncated, autoreset != 0)
+ * also fill feat_cur[pos-K+1 .. pos-1] and, ahead of the next step's window fill,
+ * feat_other[pos-K+2 .. pos]. Precondition: both feature windows [pos-K .. pos-1] hold the
+ * previous call's result (a fresh start: f16env_features_strided over both windows after a
+ * step, then this call with transform = 0, which makes only the ahead fills). Replaces the
+ * per-step f16env_features_strided over the whole (N, K, 15) view (features.py:37-67 per
+ * frame, LMA_features.py:757-765 over the stack). */
 int f16env_features_window_step(void* stream, int64_t n, int32_t K, int32_t pos, const float* hist_cur,
-                                const float* hist_other, int64_t pos_stride, int64_t env_stride, float* feat_cur,
-                                float* feat_other, const uint8_t* terminated, const uint8_t* truncated,
-                                uint8_t* prev_done, int32_t autoreset);
+                                int64_t pos_stride, int64_t env_stride, float* feat_cur, float* feat_other,
+                                const uint8_t* terminated, const uint8_t* truncated, int32_t autoreset,
+                                int32_t transform);
 
 /* Render/telemetry poses, replacing the state -> Viewer transform of
  * jsbsim_gym.py:381-415 (JSBSimEnv.render) for every env at once, float32:

@@ -69,7 +69,8 @@ def test_feature_window_equals_full_transform(gpu, c):
             checked += 1
     assert checked > 30
     calls = e.feature_window_calls
-    assert calls["incremental"] > calls["full"], calls
+    # without auto-reset the caller's resets (most steps here) make whole-window transforms
+    assert calls["incremental"] > (calls["full"] if c["autoreset"] else 5), calls
     e.close()
 
 
