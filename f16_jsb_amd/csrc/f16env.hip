@@ -1930,25 +1930,26 @@ __global__ __launch_bounds__(256) void f16_feature_window_kernel(FeatWinArgs a) 
     if (e < nb) frame_features_part(sIn + e * FW_IN, sY + e * FEAT_OUT, w);
     __syncthreads();
   }
-  if (done && a.K > 1) {  // rare: the reset lanes' window fills (rows below p in fx, ahead in fy)
-    // wave w writes features j = w, w+4, ... of env e
-    float v[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const int j = w + 4 * i;
-      v[i] = j < FEAT_OUT ? (a.transform ? sY[e * FEAT_OUT + j] : a.fx[(int64_t)a.p * rowN + k * FEAT_OUT + j]) : 0.0f;
-    }
-    for (int r = a.p - a.K + 1; r <= a.p; ++r) {
-      float* dx = a.fx + (int64_t)r * rowN + k * FEAT_OUT;
-      float* dy = a.fy + (int64_t)r * rowN + k * FEAT_OUT;
-      const bool wx_ = r < a.p, wy_ = r > a.p - a.K + 1 && (r < a.p || !a.transform);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const int j = w + 4 * i;
-        if (j < FEAT_OUT) {
-          if (wx_) dx[j] = v[i];
-          if (wy_) dy[j] = v[i];
-        }
+  // rare: the window fills of the block's reset envs (rows below p in fx, ahead in fy). Every
+  // wave sees the same done mask (env e = lane); wave w takes every 4th reset env and spreads
+  // its (row, feature) pairs over its 64 lanes: whole-wave stores, not one lane per env walking
+  // 2K-2 rows a page apart (gpurun fw r04: +3.3 us at K = 10 for 0.13 % of lanes reset)
+  const uint64_t dm = __ballot(done);
+  if (dm && a.K > 1) {
+    const int nrx = a.K - 1;                          // fx rows p-K+1 .. p-1
+    const int nry = a.transform ? a.K - 2 : a.K - 1;  // fy rows p-K+2 .. p-1 (.. p without transform)
+    const int items = (nrx + nry) * FEAT_OUT;
+    int idx = 0;
+    for (uint64_t m = dm; m; m &= m - 1, ++idx) {
+      if ((idx & 3) != w) continue;
+      const int ee = __builtin_ctzll(m);
+      const int64_t kk = k0 + ee;
+      for (int it = e; it < items; it += 64) {
+        const int ri = it / FEAT_OUT, j = it - ri * FEAT_OUT;
+        const float v = a.transform ? sY[ee * FEAT_OUT + j] : a.fx[(int64_t)a.p * rowN + kk * FEAT_OUT + j];
+        float* d = ri < nrx ? a.fx + (int64_t)(a.p - a.K + 1 + ri) * rowN
+                            : a.fy + (int64_t)(a.p - a.K + 2 + (ri - nrx)) * rowN;
+        d[kk * FEAT_OUT + j] = v;
       }
     }
   }
