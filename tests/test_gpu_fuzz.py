@@ -8,7 +8,8 @@ trips, the NaN guard and the observation-bounds diagnostic, 1, 2 or 4 FDM frames
 Each case runs three handles on identical inputs for 15 steps:
   * the windowed layout against the contiguous one: bit-identical observations, rewards, flags,
     episode statistics and terminal observations (one per-expression FMA contraction,
-    build.py -ffp-contract=on);
+    build.py -ffp-contract=on); and the windowed handle's feature window (obs_features) equal
+    to the whole-window feature transform;
   * the contiguous layout against the CPU oracle (oracle/f16ref.c): done flags and episode lengths
     bit-exact, rewards 2e-3, newest frames within the random-action tolerance of
     tests/test_gpu_parity.py (the cfg5 transonic tail statistically, as test_gpu_production.py);
@@ -61,6 +62,7 @@ def _np(x):
 def test_fuzz_layouts_and_oracle(gpu, case):
     import torch
     from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.features import features
     c = case
     n, k = c["n"], c["k"]
     kw = dict(stack_k=k, seed=c["seed"], max_steps=c["max_steps"], cfg5=c["cfg5"], down_sample=c["down_sample"])
@@ -110,6 +112,8 @@ def test_fuzz_layouts_and_oracle(gpu, case):
         np.testing.assert_array_equal(_np(sb.rew), _np(sa.rew), err_msg="rew @%d" % t)
         np.testing.assert_array_equal(_np(sb.terminated), _np(sa.terminated), err_msg="term @%d" % t)
         np.testing.assert_array_equal(_np(sb.truncated), _np(sa.truncated), err_msg="trunc @%d" % t)
+        if t % 4 != 3:  # the feature window (steps without a call in between: whole-window restarts)
+            assert torch.equal(b.obs_features(), features(sb.obs)), "feature window @%d" % t
         te_a, tr_a = _np(sa.terminated).astype(bool), _np(sa.truncated).astype(bool)
         d = te_a | tr_a
         if d.any() and c["autoreset"]:
