@@ -510,7 +510,8 @@ class F16Envs:
         frame; LMA_features.py:757-765 over the stack), equal bit for bit to
         features.features(self.obs). Windowed layout: kept in two feature histories beside the
         frame histories ([T][N][17] per parity, position-major; the result is a view, valid
-        until the next step as self.obs), so a call after each step transforms one frame per
+        until the first call after the next step, which writes the other parity's rows), so a
+        call after each step transforms one frame per
         env (f16env_features_window_step) instead of K. The first call, a call after a reset,
         set_state, set_obs or rollout_random, the call after the step that follows one of
         those, and a call after a step not followed by a call transform both whole windows.
