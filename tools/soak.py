@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Soak run of the bench's own configurations: many thousands of steps at BASELINE sizes,
 window restarts and reset-cache refills included, with the NaN guard and the observation-bounds
-diagnostic on; with F16ENV_LIB pointing at libf16env_debug.so the kernels also record every
+diagnostic on, the feature window (F16Envs.obs_features) after every step; with F16ENV_LIB pointing at libf16env_debug.so the kernels also record every
 index / range invariant they find violated (f16env_debug_checks). Prints one JSON line.
 
     python tools/soak.py [--steps3 N] [--steps5 N]
@@ -32,10 +32,18 @@ def soak(n, steps, cfg5, seed):
     spread_phases(e, argparse.Namespace(seed=seed, burn_in=None), e.device)
     ep0 = float(e.get_state()[:, F16C_EP_COUNT].sum())
     a = torch.empty((n, 4), dtype=torch.float32, device=e.device)
+    from f16_jsb_amd.features import features
+    fw_checks = fw_mismatch = 0
     t0 = time.time()
     for t in range(steps):
         e.sample_actions(seed + 11, t, out=a)
         out = e.step(a)
+        # the feature window after every step (window restarts and resets included), checked
+        # against the whole-window transform every 997 steps
+        fv = e.obs_features()
+        if t % 997 == 996:
+            fw_checks += 1
+            fw_mismatch += int(not torch.equal(fv, features(out.obs)))
     torch.cuda.synchronize()
     wall = time.time() - t0
     finite = bool(torch.isfinite(out.obs).all())
@@ -45,6 +53,7 @@ def soak(n, steps, cfg5, seed):
     r = {"envs": n, "steps": steps, "cfg5": cfg5, "kernel": e.step_kernel_name, "auto_resets": int(resets),
          "nonfinite_quarantined": e.nonfinite_count, "obs_out_of_bounds": e.obs_bounds_count,
          "final_obs_finite": finite, "debug_build": bool(is_debug), "violations": int(v.value),
+         "feature_window": {"checks": fw_checks, "mismatches": fw_mismatch, "calls": dict(e.feature_window_calls)},
          "wall_s": round(wall, 2)}
     e.close()
     return r
