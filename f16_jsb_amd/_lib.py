@@ -64,6 +64,7 @@ def lib():
     _set(L, "f16env_window_clear_fresh", [vp, vp], i32)
     _set(L, "f16env_window_bind", [vp, vp, vp, i64, vp, vp, vp, vp, vp], i32)
     _set(L, "f16env_window_step_bound", [vp, vp, vp, i32, i32], i32)
+    _set(L, "f16env_window_feature_bind", [vp, vp, vp], i32)
     _set(L, "f16env_step_window_nt", [vp], i32)
     L.f16env_get_state.argtypes = [vp, vp, vp]
     L.f16env_nonfinite_count.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -122,7 +123,7 @@ EXPORTED_SYMBOLS = (
     "f16env_state_bytes_per_env", "f16env_reset", "f16env_step", "f16env_step_rollout", "f16env_nonfinite_count", "f16env_obs_bounds_count", "f16env_debug_checks", "f16env_rollout_random",
     "f16env_step_window", "f16env_reset_window", "f16env_window_restart", "f16env_step_window_waves_per_simd",
     "f16env_step_mode", "f16env_features_strided", "f16env_features_window_step", "f16env_set_window_order", "f16env_window_clear_fresh",
-    "f16env_window_bind", "f16env_window_step_bound", "f16env_step_window_nt", "f16env_window_step_rollout",
+    "f16env_window_bind", "f16env_window_step_bound", "f16env_window_feature_bind", "f16env_step_window_nt", "f16env_window_step_rollout",
     "f16env_window_rollout_random", "f16env_bootstrap_timeouts", "f16env_bootstrap_stash", "f16env_bootstrap_apply", "f16env_abi_version",
     "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end", "f16env_profile_times",

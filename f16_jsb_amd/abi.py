@@ -139,6 +139,7 @@ def algorithmic_bytes_per_env_step(stack_k: int, state_bytes: int, layout: str =
 
 
 F16_SLOT_CLIP = 0x1  # the env steps np.clip(act, low, high); the slot keeps act unclipped
+F16_SLOT_FEATURE_WINDOW = 0x2  # the windowed rollout-slot step also updates the bound feature histories
 
 
 class RolloutSlot(ctypes.Structure):

@@ -591,6 +591,10 @@ struct StepArgs {
   int64_t wenv;                // floats between envs (position-major: 16; env-major: T * 16)
   int32_t wpos;                // newest frame position p (window = p-K+1 .. p)
   int32_t half_delay;          // HALF builds (experiment): cycles the second half of the grid waits
+  // the feature window in the rollout-slot build (F16_SLOT_FEATURE_WINDOW): the feature
+  // histories [T][N][17] of this step's parity (fwx) and the other (fwy); nullptr: none
+  float* fwx;
+  float* fwy;
   // cfg5 modes, windowed layout: the reset cache (f16_ic_fill_kernel): per lane the state and
   // frame 0 (without the goal) of its NEXT reset, ICC_COLS columns; c == nullptr: deferred
   // resets by f16_reset_done_kernel instead
@@ -984,6 +988,53 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         const float* fr = reset_now ? f0 : f;
 #pragma unroll
         for (int c = 0; c < F16_OBS_DIM; ++c) a.r_next_frame[k * F16_OBS_DIM + c] = fr[c];
+      }
+    }
+    if (ROLL && a.fwx) {
+      // the feature window (f16_feature_window_kernel's invariant, written here instead of by a
+      // second launch): fx[p] = fy[p] = features of wx[p]; a lane reset now also fills
+      // fx[p-K+1 .. p-1] and, ahead of the next step's window fill, fy[p-K+2 .. p-1]. The
+      // wave's 64 rows (64 * 17 contiguous floats per history) leave through its staging area
+      // (free after the frame stores) as float4.
+      const int64_t rowN = a.E.n * FEAT_OUT;
+      float y[FEAT_OUT];
+      if (live) frame_features(reset_now ? f0 : f, y);
+      if (rows == EPW) {
+        float* sf = stg;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < FEAT_OUT; ++j) sf[lane * FEAT_OUT + j] = y[j];
+        __builtin_amdgcn_wave_barrier();
+        float* gx = a.fwx + (int64_t)p * rowN + row0 * FEAT_OUT;
+        float* gy = a.fwy + (int64_t)p * rowN + row0 * FEAT_OUT;
+        if (((((uintptr_t)gx) | ((uintptr_t)gy)) & 15) == 0) {
+          for (int u = lane; u < 64 * FEAT_OUT / 4; u += 64) {
+            const float4 v = reinterpret_cast<const float4*>(sf)[u];
+            reinterpret_cast<float4*>(gx)[u] = v;
+            reinterpret_cast<float4*>(gy)[u] = v;
+          }
+        } else {
+          for (int u = lane; u < 64 * FEAT_OUT; u += 64) {
+            gx[u] = sf[u];
+            gy[u] = sf[u];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (live) {
+#pragma unroll
+        for (int j = 0; j < FEAT_OUT; ++j) {
+          a.fwx[(int64_t)p * rowN + k * FEAT_OUT + j] = y[j];
+          a.fwy[(int64_t)p * rowN + k * FEAT_OUT + j] = y[j];
+        }
+      }
+      if (reset_now && K > 1) {  // rare
+        for (int r = p - K + 1; r < p; ++r) {
+#pragma unroll
+          for (int j = 0; j < FEAT_OUT; ++j) {
+            a.fwx[(int64_t)r * rowN + k * FEAT_OUT + j] = y[j];
+            if (r > p - K + 1) a.fwy[(int64_t)r * rowN + k * FEAT_OUT + j] = y[j];
+          }
+        }
       }
     }
     F16_STAMP(stamps, ST_COPY);
@@ -2060,6 +2111,7 @@ struct f16env {
   int win_nt;         // windowed step: non-temporal output stores
   int win_half;       // experiment (F16ENV_HALF=1): 32 envs per wave, f16_step_win_half_kernel
   int half_delay;     // ... and the second half of its grid starting this many cycles late
+  float* fw[2];       // f16env_window_feature_bind: the feature histories (parity 0, 1)
   struct {            // f16env_window_bind: the buffers of f16env_window_step_bound
     float* hist[2];
     int64_t T;
@@ -2559,6 +2611,15 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
     feat = slot->features;
     if ((a.r_next_frame && ((uintptr_t)a.r_next_frame & 3) != 0) || (a.r_act && ((uintptr_t)a.r_act & 15) != 0))
       return set_err(-1, "rollout slot next_frame must be 4-byte and actions 16-byte aligned");
+    if (slot->flags & F16_SLOT_FEATURE_WINDOW) {
+      if (!h->fw[0] || !h->fw[1]) return set_err(-1, "F16_SLOT_FEATURE_WINDOW: f16env_window_feature_bind first");
+      if (hist_cur != h->wb.hist[0] && hist_cur != h->wb.hist[1])
+        return set_err(-1, "F16_SLOT_FEATURE_WINDOW: the step's histories must be the bound ones");
+      if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period <= 0)
+        return set_err(-1, "F16_SLOT_FEATURE_WINDOW: not with the deferred-reset step (F16ENV_ICC_PERIOD=0)");
+      const int b = hist_cur == h->wb.hist[0] ? 0 : 1;
+      a.fwx = h->fw[b]; a.fwy = h->fw[b ^ 1];
+    }
   }
   int64_t P, Q;  // floats between positions, between envs
   window_strides(h, T, P, Q);
@@ -2639,6 +2700,14 @@ int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float*
   h->wb.hist[0] = hist0; h->wb.hist[1] = hist1; h->wb.T = T;
   h->wb.rew = rew; h->wb.term = terminated; h->wb.trunc = truncated;
   h->wb.ep_ret = ep_return; h->wb.ep_len = ep_len;
+  return 0;
+}
+
+int f16env_window_feature_bind(f16env_t h, float* feat0, float* feat1) {
+  if (!h) return set_err(-1, "null handle");
+  if ((!feat0) != (!feat1) || (feat0 && feat0 == feat1)) return set_err(-1, "two distinct feature histories (or none)");
+  if (((((uintptr_t)feat0) | ((uintptr_t)feat1)) & 3) != 0) return set_err(-1, "feature histories must be float-aligned");
+  h->fw[0] = feat0; h->fw[1] = feat1;
   return 0;
 }
 

@@ -22,7 +22,7 @@ import numpy as np
 from . import spaces
 from ._lib import F16EnvError, check, lib
 from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
-                  F16_FLAG_OBS_CHECK, F16_SLOT_CLIP,
+                  F16_FLAG_OBS_CHECK, F16_SLOT_CLIP, F16_SLOT_FEATURE_WINDOW,
                   F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
@@ -119,7 +119,7 @@ class F16Envs:
             self._step_op = -1    # the last op that was a step
             self._feat_op = -1    # the op the feature windows describe
             self._feat_prev_ok = False  # the feature windows hold the last step's ahead fills
-            self.feature_window_calls = {"incremental": 0, "full": 0}
+            self.feature_window_calls = {"incremental": 0, "full": 0, "fused": 0}
         else:
             self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
         self._cur = 0
@@ -374,10 +374,11 @@ class F16Envs:
                            _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(features), _ptr(next_frame),
                            F16_SLOT_CLIP if clip else 0, 0)
         if self.window:
+            fw = self._fused_features(slot)
             s, cur, p = self._advance()
             check(lib().f16env_window_step_rollout(self._h, s, ctypes.byref(slot), _ptr(act), cur, p),
                   "f16env_window_step_rollout")
-            return self._advanced(cur, p)
+            return self._fused_done(fw, self._advanced(cur, p))
         prev = self._obs[self._cur]
         nxt = self._obs[self._cur ^ 1]
         check(lib().f16env_step_rollout(self._h, self._stream(), ctypes.byref(slot), _ptr(act), _ptr(prev), _ptr(nxt),
@@ -391,16 +392,30 @@ class F16Envs:
         collect_rollout validates its buffers once per rollout and moves the slot's row
         addresses itself (the per-step host cost is then the launch, not the checks)."""
         if self.window:
+            fw = self._fused_features(slot)
             s, cur, p = self._advance()
             check(lib().f16env_window_step_rollout(self._h, s, ctypes.byref(slot), act_ptr, cur, p),
                   "f16env_window_step_rollout")
-            return self._advanced(cur, p)
+            return self._fused_done(fw, self._advanced(cur, p))
         cur = self._cur
         nxt = self._obs[cur ^ 1]
         check(lib().f16env_step_rollout(self._h, self._stream_int(), ctypes.byref(slot), act_ptr, self._obs_ptr[cur],
                                         self._obs_ptr[cur ^ 1], *self._out_ptr, None, None), "f16env_step_rollout")
         self._cur = cur ^ 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
+
+    def _fused_features(self, slot) -> bool:
+        """Whether this rollout-slot step keeps the feature window itself (F16_SLOT_FEATURE_WINDOW:
+        the windows are current, so the step's epilogue brings them to its new position)."""
+        fw = self._fh is not None and self._feat_prev_ok and self._feat_op == self._op
+        slot.flags = (slot.flags | F16_SLOT_FEATURE_WINDOW) if fw else (slot.flags & ~F16_SLOT_FEATURE_WINDOW)
+        return fw
+
+    def _fused_done(self, fw: bool, out: StepOut) -> StepOut:
+        if fw:
+            self._feat_op = self._op
+            self.feature_window_calls["fused"] += 1
+        return out
 
     def rollout_random(self, seed: int, step0: int, n_steps: int, frames, actions, rewards, next_start,
                        last_start) -> None:
@@ -512,7 +527,9 @@ class F16Envs:
         frame histories ([T][N][17] per parity, position-major; the result is a view, valid
         until the first call after the next step, which writes the other parity's rows), so a
         call after each step transforms one frame per
-        env (f16env_features_window_step) instead of K. The first call, a call after a reset,
+        env (f16env_features_window_step) instead of K, and a rollout-slot step (step_rollout,
+        collect_rollout) keeps them in its own epilogue (F16_SLOT_FEATURE_WINDOW: no launch
+        here at all). The first call, a call after a reset,
         set_state, set_obs or rollout_random, the call after the step that follows one of
         those, and a call after a step not followed by a call transform both whole windows.
         Contiguous layout: features(self.obs)."""
@@ -525,6 +542,8 @@ class F16Envs:
             # (positions outside the window are written before they are read)
             self._fh = t.empty((2, self.T, n, FEATURES_DIM), dtype=t.float32, device=self.device)
             self._fh_ptr = (self._fh[0].data_ptr(), self._fh[1].data_ptr())
+            # rollout-slot steps update them in their epilogue (F16_SLOT_FEATURE_WINDOW)
+            check(L.f16env_window_feature_bind(self._h, *self._fh_ptr), "f16env_window_feature_bind")
             self._fviews = [[None] * self.T for _ in range(2)]
         cur, p = self._cur, self._p
         if self._feat_op != self._op:

@@ -48,7 +48,8 @@ extern "C" {
  * windowed layout's FRESH mark; the rollout slot gained next_frame / flags (F16_SLOT_CLIP);
  * f16env_rollout_random has no stack_k / mode limits; new f16env_window_step_rollout,
  * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_bootstrap_stash,
- * f16env_bootstrap_apply, f16env_features_window_step, f16env_abi_version. */
+ * f16env_bootstrap_apply, f16env_features_window_step, f16env_window_feature_bind
+ * (+ F16_SLOT_FEATURE_WINDOW), f16env_abi_version. */
 #define F16ENV_ABI_VERSION 3
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
@@ -249,6 +250,9 @@ int f16env_step_window(f16env_t h, void* stream, const float* act, float* hist_c
 int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float* rew, uint8_t* terminated,
                        uint8_t* truncated, double* ep_return, int32_t* ep_len);
 int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos);
+/* The two feature histories ([T][N][17] float32, parity 0 and 1; T as f16env_window_bind) that
+ * rollout-slot steps with F16_SLOT_FEATURE_WINDOW update (NULL, NULL: unbind). */
+int f16env_window_feature_bind(f16env_t h, float* feat0, float* feat1);
 /* f16env_reset for windowed observations: K copies of frame 0 into hist_cur's window ending at
  * pos (mask / goals / ic as f16env_reset; jsbsim_gym.py:289-331 x N). */
 int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,
@@ -286,10 +290,15 @@ int f16env_step_window_nt(f16env_t h);
  *   features   N x K x 17 float: policy features of the returned observation (below)
  *   flags      F16_SLOT_CLIP: the env steps np.clip(act, low, high) over the action Box
  *              (on_policy_algorithm.py:216; numpy's clip ufunc semantics, NaN passes), while
- *              `actions` keeps act unclipped
+ *              `actions` keeps act unclipped; F16_SLOT_FEATURE_WINDOW (windowed layout, ABI 3):
+ *              the step also updates the feature histories bound by f16env_window_feature_bind
+ *              exactly as f16env_features_window_step (transform 1) would after it -- the
+ *              feature window in the step's epilogue, no second launch; the caller keeps the
+ *              same precondition (both feature windows current before the step)
  * act == NULL draws the actions in-kernel from the f16env_sample_actions stream
  * (act_seed, act_step), bit-identical to f16env_sample_actions followed by f16env_step. */
 #define F16_SLOT_CLIP 0x1
+#define F16_SLOT_FEATURE_WINDOW 0x2
 typedef struct f16env_rollout_slot {
   uint64_t act_seed, act_step;
   float* frame;

@@ -74,6 +74,39 @@ def test_feature_window_equals_full_transform(gpu, c):
     e.close()
 
 
+@pytest.mark.parametrize("k,order,cfg5", [(4, "position", False), (10, "env", False), (3, "position", True),
+                                           (1, "position", False)])
+def test_feature_window_fused_in_rollout_steps(gpu, k, order, cfg5):
+    """Rollout-slot steps (step_rollout, in-kernel or policy actions, clipped) keep the feature
+    window in their epilogue (F16_SLOT_FEATURE_WINDOW): after each, obs_features launches
+    nothing and equals the whole-window transform; mixed with plain steps (incremental kernel),
+    short TimeLimits (resets every few steps), restarts (T = 2K+1) and a caller reset."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.features import features
+    n = 777
+    e = F16Envs(n, stack_k=k, seed=5, max_steps=5, cfg5=cfg5, obs_layout="window", history=2 * k + 1,
+                window_order=order)
+    e.reset()
+    rng = np.random.default_rng(k)
+    for i in range(50):
+        r = rng.random()
+        if i == 25:
+            e.reset(mask=torch.as_tensor(rng.random(n) < 0.5))
+        elif r < 0.4:
+            e.step_rollout(9, i)
+        elif r < 0.8:
+            act = (torch.randn((n, 4), device=gpu) * 1.5).contiguous()
+            e.step_rollout(9, i, policy_actions=act, clip=True)
+        else:
+            e.step(e.sample_actions(4, i))
+        got = e.obs_features()
+        assert torch.equal(got, features(e.obs)), i
+    calls = e.feature_window_calls
+    assert calls["fused"] > 25 and calls["full"] <= 4, calls
+    e.close()
+
+
 def test_feature_window_contiguous_layout(gpu):
     """The contiguous layout has no feature histories: obs_features is the transform of obs."""
     import torch

@@ -2,7 +2,8 @@
 K = 4 and K = 10, `steps` steps each followed by F16Envs.obs_features() (the incremental
 f16_feature_window_kernel), then `steps` steps each followed by the whole-window transform
 (features(envs.obs), f16_features_strided_kernel), so the summary holds both kernels' average
-durations side by side. Prints one JSON line with the host-driven ms per step of each form.
+durations side by side; then rollout-slot steps (step_rollout with policy actions) without and
+with obs_features after each (the feature window kept in the step's epilogue). Prints one JSON line with the host-driven ms per step of each form.
 
     rocprofv3 --kernel-trace --stats -d gpurun_out/fw -o run --output-format csv -- python3 tools/fw_probe.py
 """
@@ -28,15 +29,22 @@ def main(steps=300):
         buf = torch.empty((65536, k, 17), dtype=torch.float32, device=dev)
         s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         res = {}
-        for name in ("plain", "window", "whole"):
+        for name in ("plain", "window", "whole", "rollout_step", "rollout_step_fused"):
+            roll = name.startswith("rollout")
             for i in range(20):
-                e.step(acts[i % 8])
-                if name == "window":
+                if roll:
+                    e.step_rollout(7, i, policy_actions=acts[i % 8])
+                else:
+                    e.step(acts[i % 8])
+                if name in ("window", "rollout_step_fused"):
                     e.obs_features()  # (the first call allocates the feature histories)
             s.record()
             for i in range(steps):
-                o = e.step(acts[i % 8]).obs
-                if name == "window":
+                if roll:  # the rollout-slot step: with the feature window current, it keeps it
+                    o = e.step_rollout(7, i, policy_actions=acts[i % 8]).obs
+                else:
+                    o = e.step(acts[i % 8]).obs
+                if name in ("window", "rollout_step_fused"):
                     e.obs_features()
                 elif name == "whole":
                     features(o, buf)
