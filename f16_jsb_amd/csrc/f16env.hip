@@ -1019,6 +1019,22 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
             gy[u] = sf[u];
           }
         }
+        // the window fills of the wave's reset lanes (rare), each lane's (row, feature) pairs
+        // spread over the whole wave from the staging area (as f16_feature_window_kernel)
+        const uint64_t rm = __ballot(reset_now);
+        if (rm && K > 1) {
+          const int items = (2 * K - 3) * FEAT_OUT;  // fx rows p-K+1 .. p-1, fy rows p-K+2 .. p-1
+          for (uint64_t m = rm; m; m &= m - 1) {
+            const int ee = __builtin_ctzll(m);
+            const int64_t kk = row0 + ee;
+            for (int it = lane; it < items; it += 64) {
+              const int ri = it / FEAT_OUT, j = it - ri * FEAT_OUT;
+              float* d = ri < K - 1 ? a.fwx + (int64_t)(p - K + 1 + ri) * rowN
+                                    : a.fwy + (int64_t)(p - K + 2 + (ri - (K - 1))) * rowN;
+              d[kk * FEAT_OUT + j] = sf[ee * FEAT_OUT + j];
+            }
+          }
+        }
         __builtin_amdgcn_wave_barrier();
       } else if (live) {
 #pragma unroll
@@ -1027,7 +1043,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
           a.fwy[(int64_t)p * rowN + k * FEAT_OUT + j] = y[j];
         }
       }
-      if (reset_now && K > 1) {  // rare
+      if (rows != EPW && reset_now && K > 1) {  // a partial wave's reset lanes: one lane each
         for (int r = p - K + 1; r < p; ++r) {
 #pragma unroll
           for (int j = 0; j < FEAT_OUT; ++j) {
