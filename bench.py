@@ -68,7 +68,67 @@ def parse():
     ap.add_argument("--burn-in", type=int, default=None,
                     help="untimed steps after the phase spread (default: max_steps = 1200) so the timed window "
                          "sees the steady-state episode mix (crashes, goals, truncations, auto-resets)")
+    # test hooks (tests/test_bench_launch.py, tests/test_gpu_bench_legs.py)
+    ap.add_argument("--fail-leg", default=None,
+                    help="raise inside this side leg (forced failure: the line gets legs_failed, exit 1)")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="ranks only join the process group (gloo) and rank 0 prints the launch fields: "
+                         "checks the --gpus N launcher without a GPU")
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1, help="with --launch-selftest: this rank exits 3")
     return ap.parse_args()
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed launcher: start the N
+    ranks as children of `python -m torch.distributed.run` (one process per GPU, rendezvous on
+    127.0.0.1) and relay rank 0's JSON line. This process makes no GPU call (torch is not even
+    imported here) and never exec's: it waits for the launcher, forwards the ranks' other
+    output to stderr as it arrives, and exits non-zero when any rank failed or no line came."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    print("[bench] launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for ln in proc.stdout:
+        if ln.startswith('{"metric"'):
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc != 0:
+        print("[bench] a rank failed (launcher exit %d)" % rc, file=sys.stderr, flush=True)
+        return rc if rc > 0 else 1
+    if line is None:
+        print("[bench] rank 0 printed no result line", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def launch_selftest(args, world, rank):
+    """--launch-selftest: the rank side of the launcher check -- join the group over gloo, agree
+    on the world size, rank 0 prints the line's launch fields (no GPU, no kernels)."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if rank == args.selftest_fail_rank:
+        sys.exit(3)
+    dist.barrier()
+    envs = args.envs or 65536
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "selftest": True,
+                          "ranks_joined": int(t.item()),
+                          "config": {"envs_per_gpu": envs, "global_envs": envs * world}}), flush=True)
+    dist.destroy_process_group()
 
 
 def cpu_baseline(envs, stack, seconds, cfg5=False):
@@ -788,12 +848,26 @@ def load_valu(envs, stack, kernel):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no launcher around us: start the ranks (launch_ranks makes no GPU call)
+            return launch_ranks(args, sys.argv[1:])
+        if args.gpus < 1:
+            print("[bench] --gpus must be >= 1", file=sys.stderr)
+            return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # under an external launcher the job's size is the launcher's; a mismatch would time and
+        # label the wrong configuration
+        print("[bench] WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        return 2
+    if args.launch_selftest:
+        launch_selftest(args, world, rank)
+        return 0
+    import torch
+    import torch.distributed as dist
+
     if args.dist_backend == "gloo":
         # rehearsal only: ranks share the box's GPUs round-robin (device_count does not
         # initialise the GPU); the nccl measurement keeps one GPU per rank
@@ -880,8 +954,23 @@ def main():
             envs.step(acts[t % pool])
 
     kern_ms, kern_min_ms, _ = envs.profile_kernel(second_pass, nk)
-    feat = features_bench(envs, stream)
-    telem = telemetry_bench(envs, stream)
+    legs_failed = []
+
+    def leg(name, fn, *a, **kw):
+        """A side leg beside the headline: its failure keeps the headline line but is reported
+        (`legs_failed`) and makes the run exit non-zero."""
+        try:
+            if args.fail_leg == name:
+                raise RuntimeError("forced failure (--fail-leg %s)" % name)
+            return fn(*a, **kw)
+        except Exception as ex:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            legs_failed.append(name)
+            return {"error": "%s: %s" % (type(ex).__name__, ex)}
+
+    feat = leg("features", features_bench, envs, stream)
+    telem = leg("telemetry", telemetry_bench, envs, stream)
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step, kern_min_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -889,22 +978,23 @@ def main():
     venv.close()
     del acts, warm
     torch.cuda.empty_cache()
-    sb3 = sb3_compat_bench(dev, n) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
-    cfg2 = cfg2_bench(dev) if (world == 1 and not cfg5 and not args.no_cpu_baseline) else None
-    persist = persistent_bench(dev, n, args.stack, 1000, args.seed + 6000) if (world == 1 and not cfg5) else None
+    one = world == 1 and not cfg5
+    sb3 = leg("sb3_compat", sb3_compat_bench, dev, n) if (one and not args.no_cpu_baseline) else None
+    cfg2 = leg("cfg2", cfg2_bench, dev) if (one and not args.no_cpu_baseline) else None
+    persist = leg("persistent", persistent_bench, dev, n, args.stack, 1000, args.seed + 6000) if one else None
     other = "contiguous" if args.obs_layout == "window" else "window"
-    layouts = layout_leg(dev, args, other) if (world == 1 and not cfg5) else None
+    layouts = leg("layouts", layout_leg, dev, args, other) if one else None
     rollout = None
     if not cfg5 and args.rollout_envs > 0 and args.rollout_steps > 0:
-        try:  # a side leg: its failure (e.g. a collective error at N > 1) must not lose the headline
-            rollout = rollout_bench(args, dev, rank, world)
-        except Exception as ex:  # noqa: BLE001
-            rollout = {"error": "%s: %s" % (type(ex).__name__, ex)}
-    cfg1 = cfg1_hip_bench(dev) if (world == 1 and not cfg5) else None
+        rollout = leg("rollout", rollout_bench, args, dev, rank, world)
+    cfg1 = leg("cfg1_hip", cfg1_hip_bench, dev) if one else None
 
     if rank != 0:
         dist.destroy_process_group()
-        return
+        if legs_failed:
+            print("[bench] rank %d: legs failed: %s" % (rank, ", ".join(legs_failed)), file=sys.stderr, flush=True)
+            return 1
+        return 0
     total_env_steps = n * world * args.steps
     value = total_env_steps / elapsed
     # roofline bytes: what this layout's step kernel must move per env step (window: state read
@@ -1008,11 +1098,16 @@ def main():
                                             "region_ms_per_step": round(gpu_ms_per_step, 5)},
                           other: layouts}
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.stack, args.cpu_seconds, cfg5)
+        out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, n, args.stack, args.cpu_seconds, cfg5)
+    out["legs_failed"] = legs_failed
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if legs_failed:
+        print("[bench] legs failed: %s" % ", ".join(legs_failed), file=sys.stderr, flush=True)
+        return 1
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

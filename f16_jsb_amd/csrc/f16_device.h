@@ -49,7 +49,7 @@ __device__ unsigned int g_f16_violations;
 // wave by lane 0. The production build compiles every F16_STAMP to nothing.
 enum StampSection {
   ST_LOAD = 0, ST_PROP, ST_DERIVE, ST_ATM, ST_FCS, ST_AUX, ST_ENGINE, ST_AERO, ST_ACCEL,
-  ST_FRAME_OBS, ST_REWARD, ST_RESET, ST_SYNC, ST_COPY, ST_STORE, ST_N
+  ST_FRAME_OBS, ST_REWARD, ST_RESET, ST_SYNC, ST_COPY, ST_STORE, ST_ENVPRE, ST_N
 };
 #ifdef F16_STAMPS
 struct Stamps {

@@ -765,6 +765,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     }
     earth_angle(L.epa, ce, se);
     A = alt_ref(L, ce, se);  // exact geodetic altitude once per env step
+    F16_STAMP(stamps, ST_ENVPRE);
     // 256-register windowed builds: the env fields the frames never read (goal, last distance,
     // step, episode count and return) wait in the wave's LDS stash instead of VGPRs, which the
     // frame loop needs (they were part of what spilled to scratch around it)
@@ -2637,6 +2638,15 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
       a.fwx = h->fw[b]; a.fwy = h->fw[b ^ 1];
     }
   }
+  // cfg5 modes: finished lanes are reset inside the step from the reset cache (period 0 or
+  // F16ENV_ICC_PERIOD=0: the deferred f16_reset_done_kernel instead)
+  const bool cache = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period > 0;
+  const bool deferred = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && !cache;
+  // the deferred reset rewrites finished lanes' windows after the step kernel, so a slot frame or
+  // features written by the step would describe the pre-reset window: rejected here, before any
+  // launch, so that a refused call leaves the device state untouched
+  if (deferred && slot && (slot->next_frame || feat))
+    return set_err(-1, "the deferred-reset windowed step (F16ENV_ICC_PERIOD=0) writes no next_frame / features");
   int64_t P, Q;  // floats between positions, between envs
   window_strides(h, T, P, Q);
   a.wx = hist_cur; a.wy = hist_other; a.wrow = P; a.wenv = Q; a.wpos = pos;
@@ -2646,9 +2656,6 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
   hipStream_t st = (hipStream_t)stream;
   int32_t* zero_next = nullptr;
   const dim3 blk(BLOCK);
-  // cfg5 modes: finished lanes are reset inside the step from the reset cache (period 0 or
-  // F16ENV_ICC_PERIOD=0: the deferred f16_reset_done_kernel instead)
-  const bool cache = h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period > 0;
   a.icc.c = nullptr; a.icc.n = a.E.n;
   if (cache) {
     if (int e = icc_prepare(h, st, h->icc_steps % h->icc_period == 0)) return e;
@@ -2678,7 +2685,7 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
     hipLaunchKernelGGL(kern, grid, blk, WIN_DYN_LDS, st, sc, a.act, tc, n, a);
   }
   HIPCHK(hipGetLastError());
-  if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && !cache) {
+  if (deferred) {
     ResetDoneArgs r;
     r.s = h->soa; r.tmpl = h->tmpl; r.done_idx = a.done_idx; r.n_done = a.n_done; r.obs = hist_cur;
     r.obs_row = Q; r.obs_off = (int64_t)(pos - a.E.K + 1) * P; r.obs_pitch = P; r.obs_slot = WPITCH;
@@ -2687,8 +2694,6 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
     const unsigned g = nblocks(a.E.n) < 64u ? nblocks(a.E.n) : 64u;
     hipLaunchKernelGGL(f16_reset_done_kernel, dim3(g), blk, 0, st, r);
     HIPCHK(hipGetLastError());
-    if (slot && (slot->next_frame || feat))
-      return set_err(-1, "the deferred-reset windowed step (F16ENV_ICC_PERIOD=0) writes no next_frame / features");
   }
   if (feat) {  // policy features of the returned observation, read in place from the window
     const int64_t blocks = ((int64_t)a.E.n * a.E.K + 255) / 256;

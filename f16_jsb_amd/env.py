@@ -426,7 +426,8 @@ class F16Envs:
         (episode starts of slots 1..T-1) and last_start (N,), and leaves the env at its
         observation after the last step (self.obs). Bit-identical to n_steps step_rollout calls.
         Any stack_k and mode (cfg5: random ICs + gusts). Windowed layout: the final observation
-        is written into both histories at a window beside the current one; no terminal
+        is written into both histories at a window beside the current one (when no such window
+        fits in the history, the current windows are first moved to its front); no terminal
         observation is kept for the last step's finished lanes."""
         T = int(n_steps)
         n = self.n
@@ -443,7 +444,17 @@ class F16Envs:
             k, p = self.k, self._p
             q = p + k if p + k < self.T else k - 1  # the output window: beside the input one
             if q - k + 1 <= p and p - k + 1 <= q:
-                raise F16EnvError("history too short for the rollout's output window (T = %d, K = %d)" % (self.T, k))
+                # (T < 3K - 1 and the window near the front): move the current windows
+                # of both histories to positions 0 .. K-1 first; the output window K .. 2K-1 then
+                # fits whenever T >= 2K (window_check's bound). The lanes' FRESH marks describe
+                # window-relative positions, so they stay valid.
+                for b in (0, 1):
+                    if self._env_major:
+                        self._hist[b, :, :k].copy_(self._hist[b, :, p - k + 1:p + 1].clone())
+                    else:
+                        self._hist[b, :k].copy_(self._hist[b, p - k + 1:p + 1].clone())
+                p = self._p = k - 1
+                q = 2 * k - 1
             check(lib().f16env_window_rollout_random(self._h, self._stream(), sd, st, T, self._cur, p, q, _ptr(frames),
                                                      _ptr(actions), _ptr(rewards), _ptr(next_start), _ptr(last_start)),
                   "f16env_window_rollout_random")

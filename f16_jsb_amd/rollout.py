@@ -136,7 +136,12 @@ def collect_rollout(envs, buf: DeviceRolloutBuffer, seed: int = 0, step0: int = 
     change during a rollout, so this is :236-245's arithmetic with one evaluation instead of one
     per step over the whole batch; "per_step": V over the step's whole batch of terminal
     observations every step (f16env_bootstrap_timeouts). The two agree bit for bit when V's value
-    for a row does not depend on the batch it is evaluated in."""
+    for a row does not depend on the batch it is evaluated in. SB3 itself evaluates each terminal
+    observation in a batch of ONE (`predict_values(terminal_obs)[0]` inside its per-env loop,
+    :236-245); both modes here evaluate a batch, so for a value head whose GEMMs round a row
+    differently at another batch size the bootstrapped rewards may differ from SB3's, and between
+    the two modes, in the last bits (tests/test_gpu_policy_rollout.py
+    test_bootstrap_modes_vs_batch_of_one bounds it); the lanes that bootstrap are the same."""
 
     dev = buf.device
     n = buf.n_envs

@@ -202,6 +202,49 @@ def test_deferred_bootstrap_equals_per_step(gpu, layout, k):
     assert trunc_boot > N // 4, trunc_boot
 
 
+def test_bootstrap_modes_vs_batch_of_one(gpu):
+    """SB3 bootstraps each truncated lane with V evaluated on ITS terminal observation
+    alone (a batch of one, on_policy_algorithm.py:236-245); both device modes evaluate a batch.
+    With an MLP value head (GEMMs: a row may round differently at another batch size) the rewards
+    of both modes agree with a batch-of-one reference to float32 rounding of V (|dr| <= 1e-5,
+    gamma V ~ O(1)), every other reward and buffer is bit-identical, and the same lanes
+    bootstrap."""
+    import torch
+    from bench import MlpActorCritic
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout
+    N, T, k, ms = 256, 24, 4, 7
+    net = MlpActorCritic(k * 15, gpu, seed=3)
+
+    def v_batch_of_one(obs):
+        return torch.cat([net.value(obs[i:i + 1]) for i in range(obs.shape[0])])
+
+    runs = {}
+    with torch.no_grad():
+        for name, mode, vf in (("one", "per_step", v_batch_of_one), ("per_step", "per_step", net.value),
+                               ("deferred", "deferred", net.value)):
+            torch.manual_seed(5)  # the policy's Gaussian draws: the same stream in every run
+            g = F16Envs(N, stack_k=k, seed=12, max_steps=ms, obs_layout="window")
+            g.reset()
+            buf = DeviceRolloutBuffer(T, N, k, gpu)
+            lv, ld = collect_rollout(g, buf, seed=5, policy_fn=net, value_fn=vf, bootstrap=mode)
+            runs[name] = {f: getattr(buf, f).clone() for f in ("frames", "actions", "rewards", "episode_starts")}
+            runs[name]["trunc"] = g.trunc.clone()
+            g.close()
+    ref = runs["one"]
+    boot = ref["episode_starts"][1:] > 0  # lanes whose episode ended (crash or truncation) at step t
+    assert int(boot.sum()) > N // 2
+    for name in ("per_step", "deferred"):
+        r = runs[name]
+        for f in ("frames", "actions", "episode_starts"):
+            assert torch.equal(r[f], ref[f]), (name, f)
+        d = (r["rewards"] - ref["rewards"]).abs()
+        assert float(d.max()) <= 1e-5, (name, float(d.max()))
+        # only bootstrapped (truncated-only) lanes can differ
+        changed = d[:-1] > 0
+        assert not bool((changed & ~boot).any()), name
+
+
 def _crash_ics(n):
     ic = np.tile(default_ic(), (n, 1))
     ic[:, 2] = np.linspace(150.0, 9000.0, n)  # low lanes crash and auto-reset during the rollout

@@ -135,6 +135,77 @@ def test_fused_rollout_step_equals_sample_step_add(gpu, n, k):
         e.close()
 
 
+@pytest.mark.parametrize("cfg5", [False, True], ids=["reference_task", "cfg5"])
+@pytest.mark.parametrize("layout", ["contiguous", "window"])
+def test_persistent_rollout_two_wave_build_matches_fused_steps(gpu, monkeypatch, cfg5, layout):
+    """the persistent rollout's 256-register build (f16_rollout_kernel<MODE, 2>, the
+    launch's pick above 4 x CUs x 64 envs; forced here by F16ENV_ROLL_OCC=2 at a small N)
+    against the fused rollout steps: bit-identical slots, final observation and state."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    from f16_jsb_amd.rollout import DeviceRolloutBuffer, collect_rollout
+    n, k, T = 1000, 4, 40
+    kw = dict(stack_k=k, seed=6, max_steps=25, obs_layout=layout, cfg5=cfg5)
+    if layout == "window":
+        kw["history"] = 3 * k + T
+    bufs, envs = [], []
+    for persistent in (False, True):
+        if persistent:
+            monkeypatch.setenv("F16ENV_ROLL_OCC", "2")
+        e = F16Envs(n, **kw)
+        e.reset()
+        b = DeviceRolloutBuffer(T, n, k, gpu)
+        _, last_d = collect_rollout(e, b, 31, persistent=persistent)
+        bufs.append((b, last_d.clone()))
+        envs.append(e)
+    monkeypatch.delenv("F16ENV_ROLL_OCC", raising=False)
+    (b0, d0), (b1, d1) = bufs
+    assert int(b0.episode_starts[1:].sum().item()) > 0, "expected auto-resets in the rollout"
+    for f in ("frames", "actions", "rewards", "episode_starts", "obs0"):
+        assert torch.equal(getattr(b0, f), getattr(b1, f)), f
+    assert torch.equal(d0, d1)
+    assert torch.equal(envs[0].obs, envs[1].obs)
+    assert torch.equal(envs[0].get_state(), envs[1].get_state())
+    for e in envs:
+        e.close()
+
+
+@pytest.mark.parametrize("order", ["position", "env"])
+@pytest.mark.parametrize("warm", [1, 2])
+def test_window_rollout_random_shortest_history(gpu, order, warm):
+    """a windowed handle at the shortest history (T = 2K) whose window sits where no
+    output window fits beside it (p in [K, 2K-2], after 1 or 2 steps): rollout_random moves the
+    windows to the front first, and matches a contiguous twin bit for bit (slots, the final
+    observation), then both keep stepping alike."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    n, k, steps = 500, 4, 6
+    a = F16Envs(n, stack_k=k, seed=8, max_steps=5)
+    b = F16Envs(n, stack_k=k, seed=8, max_steps=5, obs_layout="window", history=2 * k, window_order=order)
+    a.reset(), b.reset()
+    f32 = torch.float32
+    for t in range(warm):
+        act = a.sample_actions(3, t)
+        a.step(act), b.step(act)
+    assert k <= b._p <= 2 * k - 2
+    outs = []
+    for e in (a, b):
+        fr = torch.empty((steps, n, 15), dtype=f32, device=gpu)
+        ac = torch.empty((steps, n, 4), dtype=f32, device=gpu)
+        rw = torch.empty((steps, n), dtype=f32, device=gpu)
+        ns = torch.empty((steps - 1, n), dtype=f32, device=gpu)
+        ls = torch.empty(n, dtype=f32, device=gpu)
+        e.rollout_random(21, 10, steps, fr, ac, rw, ns, ls)
+        outs.append((fr, ac, rw, ns, ls, e.obs.clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    for t in range(20, 32):  # across restarts of the short history
+        act = a.sample_actions(3, t)
+        sa, sb = a.step(act), b.step(act)
+        assert torch.equal(sa.obs, sb.obs) and torch.equal(sa.rew, sb.rew)
+    a.close(), b.close()
+
+
 @pytest.mark.parametrize("n,k,T", [(4096, 4, 64), (777, 3, 33), (300, 8, 1), (65, 1, 20)])
 def test_persistent_rollout_matches_fused_steps(gpu, n, k, T):
     """f16env_rollout_random (the whole rollout in ONE launch, state kept on-chip, frames in an

@@ -110,6 +110,35 @@ def test_window_cfg5_deferred_resets(gpu, monkeypatch, period):
     assert _run(a, b, 30) > 512
 
 
+def test_window_deferred_reset_rollout_refused_before_launch(gpu, monkeypatch):
+    """the deferred-reset windowed step (cfg5, F16ENV_ICC_PERIOD=0) cannot write a
+    rollout slot's next_frame; the call is refused BEFORE any launch, so the state, the
+    observation and the episode bookkeeping are those of before the call, and the handle keeps
+    stepping bit-identically with a twin that never saw the refused call."""
+    import torch
+    from f16_jsb_amd._lib import F16EnvError
+    from f16_jsb_amd.env import F16Envs
+    monkeypatch.setenv("F16ENV_ICC_PERIOD", "0")
+    kw = dict(stack_k=4, seed=9, max_steps=5, obs_layout="window", history=12, cfg5=True)
+    a, b = F16Envs(300, **kw), F16Envs(300, **kw)
+    a.reset(), b.reset()
+    for t in range(1, 4):
+        act = a.sample_actions(4, t)
+        a.step(act), b.step(act)
+    s0, o0 = a.get_state().clone(), a.obs.clone()
+    nf = torch.zeros((300, 15), dtype=torch.float32, device=a.device)
+    with pytest.raises(F16EnvError, match="deferred-reset"):
+        a.step_rollout(7, 4, next_frame=nf)
+    torch.cuda.synchronize()
+    assert torch.equal(a.get_state(), s0) and torch.equal(a.obs, o0)
+    assert float(nf.abs().max()) == 0.0
+    for t in range(4, 12):  # keeps stepping as its twin (crashes / truncations at max_steps 5)
+        act = a.sample_actions(4, t)
+        sa, sb = a.step(act), b.step(act)
+        assert torch.equal(sa.obs, sb.obs) and torch.equal(sa.rew, sb.rew)
+        assert torch.equal(sa.terminated, sb.terminated) and torch.equal(sa.truncated, sb.truncated)
+
+
 def test_window_caller_resets(gpu):
     """NO_AUTORESET: finished lanes keep stepping until the caller resets them (mask)."""
     import torch

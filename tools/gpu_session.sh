@@ -68,7 +68,12 @@ for s in $STEPS; do
     jsbsim)  # is a JSBSim binding present on the box? (probe only; never installed)
       python -c "import jsbsim, sys; print('jsbsim', jsbsim.__version__)" > "$OUT/jsbsim_probe_$TAG.log" 2>&1
       echo "[session] jsbsim probe rc=$?"; tail -2 "$OUT/jsbsim_probe_$TAG.log" ;;
-    stamps) run stamp_profile 600 python tools/stamp_profile.py ;;
+    stamps) run stamp_profile_$TAG 600 python tools/stamp_profile.py ;;
+    floors)  # empty / copy / issue-cost floors, then the step's own (ds 4 / 0 / 1 / 2)
+      run floors_$TAG 120 tools/probes/floors 65536 300
+      run floors_step_$TAG 300 python tools/floors_step.py --json "$OUT/floors_step_$TAG.json" ;;
+    launch2)  # bench.py --gpus 2 with no external launcher (gloo: 2 ranks share the box's GPU)
+      run bench_launch2_$TAG 600 python bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
     iccsweep)  # cfg5 reset-cache refill period, same box
       for P in ${ICC_PERIODS:-8 16 32 64 128}; do
         F16ENV_ICC_PERIOD=$P run bench_cfg5_icc${P}_$TAG 300 python bench.py --workload cfg5 --steps ${ICC_STEPS:-300} --warmup 20 --no-cpu-baseline

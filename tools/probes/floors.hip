@@ -1,0 +1,291 @@
+// Floors for the windowed step kernel at 65 536 envs, and the issue cost
+// of the instruction forms the frame loop is made of, measured on the box:
+//   empty    an empty kernel at the step's grid (256 x 256 threads; plain, and with the step's
+//            LDS footprint), per launch: dispatch-event duration and back-to-back region time
+//   copy     a kernel that moves the step's bytes and nothing else: per env 16 state columns +
+//            the action read (272 B), 16 state columns written back non-temporal, the new frame
+//            slot written into both histories (2 x 64 B, LDS-transposed so every store
+//            instruction covers 1 KiB, as f16_step_win_nt_kernel does), reward and two flag bytes
+//            (390 B written); one lane per env (1 wave per SIMD) and 4 lanes per env (4 waves)
+//   issue    one wave per SIMD (and four) running 16-instruction bodies of one form in a loop:
+//            cycles per instruction from s_memtime (v_fma_f32 / v_pk_fma_f32 / v_pk_mul_f32,
+//            independent and dependent, v_sub_f32 with a literal, v_lshrrev + v_add3 counting,
+//            s_add interleaved with VALU, v_exp_f32)
+// Prints one JSON object per line. Every kernel ends with a vector store of its result (no
+// scalar stores anywhere).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/floors.hip -o tools/probes/floors
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+static constexpr int BLOCK = 256;
+static constexpr int NCOL = 16;
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK, 1) void k_empty() {}
+__global__ __launch_bounds__(BLOCK, 1) void k_empty_lds(float* out) {
+  extern __shared__ float dyn[];
+  if (out && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) out[0] = dyn[0];  // never taken: keeps the LDS
+}
+
+// the step's byte pattern, LPE lanes per env
+template <int LPE, bool NT>
+__global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, const float4* __restrict__ act, int64_t n,
+                                                   float* __restrict__ h0, float* __restrict__ h1, int32_t pos,
+                                                   float* __restrict__ rew, uint8_t* __restrict__ term,
+                                                   uint8_t* __restrict__ trunc) {
+  __shared__ __align__(16) float4 stg[4][64 * 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t k = t / LPE;
+  const int sub = (int)(t % LPE);
+  if (k >= n) return;
+  constexpr int CPL = NCOL / LPE;  // columns per lane
+  float4 c[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) c[j] = sc[(int64_t)(sub + LPE * j) * n + k];
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sub == 0) a = act[k];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // a trivially dependent "frame": 16 floats from what was loaded
+  float4 f[4];
+  f[0] = make_float4(c[0].x + a.x, c[0].y + a.y, c[0].z + a.z, c[0].w + a.w);
+#pragma unroll
+  for (int j = 1; j < 4; ++j) f[j] = c[j % CPL];
+  typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    float4* p = sc + (int64_t)(sub + LPE * j) * n + k;
+    const float4 v = make_float4(c[j].x + 1.0f, c[j].y, c[j].z, c[j].w);
+    if (NT) __builtin_nontemporal_store(__builtin_bit_cast(v4f, v), reinterpret_cast<v4f*>(p));
+    else *p = v;
+  }
+  float* hist[2] = {h0, h1};
+  if (LPE == 1) {
+    // the step's transposed slot stores: the wave's 64 slots are one 4 KiB block; through LDS so
+    // each store instruction writes 16 whole slots (1 KiB)
+    float4* st4 = stg[wave];
+    const int q = lane & 3, sw = (lane >> 2) & 3;
+    const int64_t row0 = k - lane;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st4[lane * 4 + (j ^ sw)] = f[j];
+      __builtin_amdgcn_wave_barrier();
+      float* dst = hist[h] + ((int64_t)pos * n + row0 + (lane >> 2)) * 16 + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * j + (lane >> 2);
+        const float4 v = st4[r * 4 + (q ^ ((r >> 2) & 3))];
+        float4* p = reinterpret_cast<float4*>(dst + (int64_t)(16 * j) * 16);
+        if (NT) __builtin_nontemporal_store(__builtin_bit_cast(v4f, v), reinterpret_cast<v4f*>(p));
+        else *p = v;
+      }
+    }
+  } else {
+    // LPE lanes per env: lane `sub` writes quarter(s) of the slot: contiguous per wave already
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      for (int j = sub; j < 4; j += LPE) {
+        float4* p = reinterpret_cast<float4*>(hist[h] + ((int64_t)pos * n + k) * 16) + j;
+        if (NT) __builtin_nontemporal_store(__builtin_bit_cast(v4f, f[j]), reinterpret_cast<v4f*>(p));
+        else *p = f[j];
+      }
+  }
+  if (sub == 0) {
+    rew[k] = f[0].x;
+    term[k] = (uint8_t)(f[0].y > 1e30f);
+    trunc[k] = (uint8_t)(f[0].z > 1e30f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// issue-cost bodies: 16 instructions of one form per iteration, ITER iterations
+typedef float f2 __attribute__((ext_vector_type(2)));
+enum Form { F_FMA, F_FMA_DEP, F_PKFMA, F_PKFMA_DEP, F_PKMUL, F_SUBLIT, F_SIGNCOUNT, F_SALU_MIX, F_EXP, F_MOV, F_N };
+static const char* FORM_NAME[F_N] = {"v_fma_f32 indep", "v_fma_f32 dep", "v_pk_fma_f32 indep", "v_pk_fma_f32 dep",
+                                     "v_pk_mul_f32 indep", "v_sub_f32 literal indep",
+                                     "sign-bit count (v_sub_f32 lit + v_lshrrev + v_add3 per 2)",
+                                     "v_fma_f32 + s_add_u32 alternating", "v_exp_f32 indep", "v_mov_b32 indep"};
+
+#define R8(X) X X X X X X X X
+template <int FORM>
+__global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long long* cyc, int iters, float seed) {
+  float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+        a7 = a0 + 7;
+  f2 p0 = {a0, a1}, p1 = {a2, a3}, p2 = {a4, a5}, p3 = {a6, a7}, p4 = p0 + 1.f, p5 = p1 + 1.f, p6 = p2 + 1.f,
+     p7 = p3 + 1.f;
+  const float m = 0.999f, b = 1e-3f;
+  const f2 pm = {m, m}, pb = {b, b};
+  uint32_t u0 = 0, u1 = 0;
+  uint32_t s0 = 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    if (FORM == F_FMA) {
+      asm volatile(R8("v_fma_f32 %0, %0, %8, %9\n v_fma_f32 %1, %1, %8, %9\n") : "+v"(a0), "+v"(a1), "+v"(a2),
+                   "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m), "v"(b));
+    } else if (FORM == F_FMA_DEP) {
+      asm volatile(R8("v_fma_f32 %0, %0, %1, %2\n v_fma_f32 %0, %0, %1, %2\n") : "+v"(a0) : "v"(m), "v"(b));
+    } else if (FORM == F_PKFMA) {
+      asm volatile(R8("v_pk_fma_f32 %0, %0, %8, %9\n v_pk_fma_f32 %1, %1, %8, %9\n") : "+v"(p0), "+v"(p1), "+v"(p2),
+                   "+v"(p3), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pm), "v"(pb));
+    } else if (FORM == F_PKFMA_DEP) {
+      asm volatile(R8("v_pk_fma_f32 %0, %0, %1, %2\n v_pk_fma_f32 %0, %0, %1, %2\n") : "+v"(p0) : "v"(pm), "v"(pb));
+    } else if (FORM == F_PKMUL) {
+      asm volatile(R8("v_pk_mul_f32 %0, %0, %8\n v_pk_mul_f32 %1, %1, %8\n") : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3),
+                   "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pm));
+    } else if (FORM == F_SUBLIT) {
+      asm volatile(R8("v_sub_f32 %0, 0x3e4ccccd, %0\n v_sub_f32 %1, 0x3f4ccccd, %1\n") : "+v"(a0), "+v"(a1), "+v"(a2),
+                   "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+    } else if (FORM == F_SIGNCOUNT) {
+      // per 2 breakpoints: 2 v_sub_f32 (literal) + v_lshrrev_b32 + v_add3_u32 (the shipped form):
+      // 4 such groups = 16 instructions
+      asm volatile(R8("v_sub_f32 %2, 0x3e4ccccd, %0\n v_lshrrev_b32 %2, 31, %2\n") : "+v"(a0), "+v"(a1), "+v"(u0),
+                   "+v"(u1));
+    } else if (FORM == F_SALU_MIX) {
+      asm volatile(R8("v_fma_f32 %0, %0, %3, %4\n s_add_u32 %2, %2, 1\n") : "+v"(a0), "+v"(a1), "+s"(s0)
+                   : "v"(m), "v"(b));
+    } else if (FORM == F_EXP) {
+      asm volatile(R8("v_exp_f32 %0, %0\n v_exp_f32 %1, %1\n") : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4),
+                   "+v"(a5), "+v"(a6), "+v"(a7));
+    } else if (FORM == F_MOV) {
+      asm volatile(R8("v_mov_b32 %0, %1\n v_mov_b32 %1, %0\n") : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4),
+                   "+v"(a5), "+v"(a6), "+v"(a7));
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const float r = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + p0.x + p1.y + p2.x + p3.y + p4.x + p5.y + p6.x + p7.y +
+                  (float)(u0 + u1 + s0);
+  const int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  out[g] = r;
+  if ((threadIdx.x & 63) == 0) cyc[g >> 6] = t1 - t0;  // a vector store from lane 0
+}
+
+// ---------------------------------------------------------------------------------------------
+template <typename F>
+static void timed(const char* name, int launches, F launch, const char* extra = "") {
+  hipEvent_t s, e;
+  CK(hipEventCreate(&s));
+  CK(hipEventCreate(&e));
+  std::vector<hipEvent_t> ev(2 * launches);
+  for (auto& x : ev) CK(hipEventCreate(&x));
+  for (int i = 0; i < 20; ++i) launch(nullptr, nullptr);
+  CK(hipDeviceSynchronize());
+  // back-to-back region (kernel + dependent-launch boundary)
+  CK(hipEventRecord(s, 0));
+  for (int i = 0; i < launches; ++i) launch(nullptr, nullptr);
+  CK(hipEventRecord(e, 0));
+  CK(hipEventSynchronize(e));
+  float region = 0;
+  CK(hipEventElapsedTime(&region, s, e));
+  // per-launch dispatch events (the interval rocprofv3's kernel trace reports)
+  for (int i = 0; i < launches; ++i) launch(ev[2 * i], ev[2 * i + 1]);
+  CK(hipDeviceSynchronize());
+  double sum = 0, mn = 1e30;
+  for (int i = 0; i < launches; ++i) {
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+    sum += ms;
+    mn = std::min(mn, (double)ms);
+  }
+  printf("{\"probe\": \"%s\", \"launches\": %d, \"kernel_us\": %.3f, \"kernel_min_us\": %.3f, \"region_us_per_launch\": %.3f%s}\n",
+         name, launches, 1e3 * sum / launches, 1e3 * mn, 1e3 * region / launches, extra);
+  fflush(stdout);
+  for (auto& x : ev) CK(hipEventDestroy(x));
+  CK(hipEventDestroy(s));
+  CK(hipEventDestroy(e));
+}
+
+template <int FORM>
+static void issue_probe(float* out, unsigned long long* cyc, int blocks, int iters) {
+  const int waves = blocks * BLOCK / 64;
+  hipLaunchKernelGGL(k_issue<FORM>, dim3(blocks), dim3(BLOCK), 0, 0, out, cyc, 8, 1.0f);  // warm
+  hipLaunchKernelGGL(k_issue<FORM>, dim3(blocks), dim3(BLOCK), 0, 0, out, cyc, iters, 1.0f);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> c(waves);
+  CK(hipMemcpy(c.data(), cyc, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  std::sort(c.begin(), c.end());
+  const double med = (double)c[waves / 2];
+  printf("{\"probe\": \"issue\", \"form\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_inst_median\": %.3f, "
+         "\"cycles_per_inst_min\": %.3f, \"insts_per_wave\": %d}\n",
+         FORM_NAME[FORM], blocks / 256, med / (16.0 * iters), (double)c[0] / (16.0 * iters), 16 * iters);
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 65536;
+  const int launches = argc > 2 ? atoi(argv[2]) : 300;
+  const int T = 124, pos = 60;
+  float4 *sc, *act;
+  float *h0, *h1, *rew, *out;
+  uint8_t *term, *trunc;
+  unsigned long long* cyc;
+  CK(hipMalloc(&sc, (size_t)n * NCOL * 16));
+  CK(hipMalloc(&act, (size_t)n * 16));
+  CK(hipMalloc(&h0, (size_t)n * T * 64));
+  CK(hipMalloc(&h1, (size_t)n * T * 64));
+  CK(hipMalloc(&rew, (size_t)n * 4));
+  CK(hipMalloc(&term, (size_t)n));
+  CK(hipMalloc(&trunc, (size_t)n));
+  CK(hipMemset(sc, 0, (size_t)n * NCOL * 16));
+  CK(hipMemset(act, 0, (size_t)n * 16));
+  const int64_t issue_threads = 4 * 65536;
+  CK(hipMalloc(&out, issue_threads * 4));
+  CK(hipMalloc(&cyc, issue_threads / 64 * 8));
+  const unsigned g1 = (unsigned)((n + BLOCK - 1) / BLOCK);
+  const size_t step_lds = 46 * 1024;  // the windowed step's LDS per workgroup (tables, template, staging)
+  char extra[160];
+  snprintf(extra, sizeof extra, ", \"envs\": %lld, \"grid\": %u", (long long)n, g1);
+  timed("empty", launches, [&](hipEvent_t a, hipEvent_t b) {
+    hipExtLaunchKernelGGL(k_empty, dim3(g1), dim3(BLOCK), 0, 0, a, b, 0u);
+  }, extra);
+  timed("empty_step_lds", launches, [&](hipEvent_t a, hipEvent_t b) {
+    hipExtLaunchKernelGGL(k_empty_lds, dim3(g1), dim3(BLOCK), (uint32_t)step_lds, 0, a, b, 0u, (float*)nullptr);
+  }, extra);
+  const double bytes = (double)n * (272 + 390);
+  auto copy_line = [&](const char* nm, int lpe, auto kern) {
+    const unsigned g = (unsigned)((n * lpe + BLOCK - 1) / BLOCK);
+    char ex[200];
+    snprintf(ex, sizeof ex, ", \"envs\": %lld, \"lanes_per_env\": %d, \"waves_per_simd\": %d, \"bytes_per_launch\": %.0f",
+             (long long)n, lpe, (int)((n * lpe / 64 + 1023) / 1024), bytes);
+    timed(nm, launches, [&](hipEvent_t a, hipEvent_t b) {
+      hipExtLaunchKernelGGL(kern, dim3(g), dim3(BLOCK), 0, 0, a, b, 0u, sc, (const float4*)act, n, h0, h1, pos, rew,
+                            term, trunc);
+    }, ex);
+  };
+  copy_line("copy_nt_1wave", 1, k_copy<1, true>);
+  copy_line("copy_nt_4wave", 4, k_copy<4, true>);
+  copy_line("copy_plain_1wave", 1, k_copy<1, false>);
+  copy_line("copy_plain_4wave", 4, k_copy<4, false>);
+  const int iters = 256;
+  for (int blocks : {256, 1024}) {
+    issue_probe<F_FMA>(out, cyc, blocks, iters);
+    issue_probe<F_FMA_DEP>(out, cyc, blocks, iters);
+    issue_probe<F_PKFMA>(out, cyc, blocks, iters);
+    issue_probe<F_PKFMA_DEP>(out, cyc, blocks, iters);
+    issue_probe<F_PKMUL>(out, cyc, blocks, iters);
+    issue_probe<F_SUBLIT>(out, cyc, blocks, iters);
+    issue_probe<F_SIGNCOUNT>(out, cyc, blocks, iters);
+    issue_probe<F_SALU_MIX>(out, cyc, blocks, iters);
+    issue_probe<F_EXP>(out, cyc, blocks, iters);
+    issue_probe<F_MOV>(out, cyc, blocks, iters);
+  }
+  return 0;
+}

@@ -12,7 +12,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DIAG = os.path.join(ROOT, "f16_jsb_amd", "libf16env_diag.so")
 NAMES = ["load+stage", "propagate", "derive", "atmosphere", "fcs", "aux", "engine", "aero", "accel",
-         "make_frame", "reward", "reset", "sync/compact", "obs copy", "state store"]
+         "make_frame", "reward", "reset", "sync/compact", "obs copy", "state store", "earth angle + alt_ref (+gust)"]
 
 
 def main():
@@ -46,9 +46,9 @@ def main():
         e.step(e.sample_actions(3, t))
     torch.cuda.synchronize()
     waves = args.envs // 64
-    buf = np.zeros((waves, 15), np.uint64)
+    buf = np.zeros((waves, len(NAMES)), np.uint64)
     n = L.f16env_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), waves)
-    assert n == 15, n
+    assert n == len(NAMES), n
     per = buf.astype(np.float64)
     tot = per.sum(axis=1)
     print("waves %d, cycles per wave step: median %.0f (min %.0f max %.0f)" % (waves, np.median(tot), tot.min(), tot.max()))
