@@ -622,12 +622,68 @@ def features_bench(envs, stream, iters=200):
               "feature_window_calls": dict(envs.feature_window_calls)}
         if g_step is not None and g_both is not None:
             fw["feature_window_ms_graph"] = round(g_both - g_step, 5)
+        fw.update(fused_step_legs(envs, act, s, e, iters))
     return {"kernel": "f16_features_strided_kernel" if envs.window else "f16_features_kernel", "frames": frames, "ms": round(ms, 5),
             "timing": "HIP-graph replay of %d launches (kernel + launch boundary)" % iters if gms is not None
             else "host-driven launches", "host_driven_ms": round(host_ms, 5),
             "frames_per_s": round(frames / (ms * 1e-3), 1), "achieved_GBps": round(gbps, 1),
             "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_frame": 128,
             "step_ms": round(plain, 5), "step_with_features_ms": round(fused, 5), **fw}
+
+
+def fused_step_legs(envs, act, s, e, iters):
+    """Beside the features leg (windowed layout, same env count and K): (1) a fused_features
+    handle, whose plain step keeps the feature window in its epilogue (f16env_window_step_ex,
+    F16_STEP_FEATURE_WINDOW), step + features per step against the plain
+    step; (2) the plain step with its actions drawn in the kernel (step(None, seed, step):
+    no sampling launch, no action read; item 5) against sample_actions + step. Host-driven
+    loops timed by HIP events on the launch stream (the region) and the kernels' own dispatch
+    events (profile_kernel)."""
+    import torch
+    from f16_jsb_amd.env import F16Envs
+    out = {}
+    fx = F16Envs(envs.n, stack_k=envs.k, seed=1, obs_layout="window", fused_features=True)
+    fx.reset()
+    for _ in range(8):  # the first step catches the feature window up, the rest fuse
+        fx.step(act)
+    n2 = iters // 2
+
+    def region(fn):
+        best = None
+        for _ in range(2):
+            torch.cuda.synchronize()
+            s.record()
+            for t in range(n2):
+                fn(t)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / n2
+            best = ms if best is None else min(best, ms)
+        return best
+
+    fused_ms = region(lambda t: fx.step(act))
+    fk, _, _ = fx.profile_kernel(lambda: [fx.step(act) for _ in range(n2)], n2)
+    out["fused_features_step_ms"] = round(fused_ms, 5)
+    out["fused_features_kernel_ms"] = round(fk, 5)
+    out["fused_features_kernel"] = lib_name(fx, 2)
+    out["fused_features_calls"] = dict(fx.feature_window_calls)
+    fx.close()
+    # in-kernel actions on the plain handle (no features): the winx build with act == NULL
+    samp = torch.empty_like(act)
+    sample_then_step = region(lambda t: (envs.sample_actions(5, t, out=samp), envs.step(samp)))
+    in_kernel = region(lambda t: envs.step(None, seed=5, step=t))
+    ik, _, _ = envs.profile_kernel(lambda: [envs.step(None, seed=5, step=t) for t in range(n2)], n2)
+    out["sample_then_step_ms"] = round(sample_then_step, 5)
+    out["in_kernel_actions_step_ms"] = round(in_kernel, 5)
+    out["in_kernel_actions_kernel_ms"] = round(ik, 5)
+    out["in_kernel_actions_kernel"] = lib_name(envs, 0)
+    return out
+
+
+def lib_name(envs, flags):
+    """The winx kernel instance f16env_window_step_ex launches for `flags` on this handle."""
+    from f16_jsb_amd._lib import lib
+    return lib().f16env_window_step_ex_kernel_name(envs._h, flags).decode()
 
 
 def telemetry_bench(envs, stream, iters=200):

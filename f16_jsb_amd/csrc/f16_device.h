@@ -407,6 +407,66 @@ __device__ __forceinline__ Seg bracket(const float (&bp)[N], const float* pairs,
   f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
   return {i, f};
 }
+// Guess-and-correct bracket (round 5): the same segment and factor as bracket(), from a guess
+// instead of a count. u(x) is a monotone map whose integer crossings b'_k (k = 1 .. N-3) lie
+// strictly inside segment k's span, bp[k] < b'_k <= bp[k+1]; the guess g = clamp(floor(u), 0,
+// N-3) is then the true 0-based segment s = #{k in 1..N-2 : bp[k] < x} or s - 1, and ONE compare
+// against the next segment's low end -- read with the guess's own (lo, 1/span) pair, both pairs
+// in one ds_read2_b64 -- settles it. ~10 VALU instead of ~3 per interior breakpoint.
+// (NaN x: the guess clamps to 0 and no compare is true, as the count gives segment 0; +-inf land
+// in the end segments, as the count.)
+template <int N>
+__device__ __forceinline__ Seg bracket_guess(const float* pairs, float x, float u) {
+  static_assert(N >= 3, "guess bracket needs an interior breakpoint");
+  const int g = (int)__builtin_amdgcn_fmed3f(u, 0.0f, (float)(N - 3));  // truncation == floor on [0, N-3]
+  const float2* P = reinterpret_cast<const float2*>(pairs);
+  const float2 p0 = P[g], p1 = P[g + 1];
+  const bool up = x > p1.x;
+  const float lo = up ? p1.x : p0.x, iv = up ? p1.y : p0.y;
+  const int i = g + 1 + (up ? 1 : 0);
+  F16_CHECK(i >= 1 && i <= N - 1, DBG_TABLE_SEGMENT);
+  float f = (x - lo) * iv;
+  f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
+  return {i, f};
+}
+// near-uniform grid: u = (x - (bp[0] + h/2)) / h with h the mean spacing, crossings at the
+// segments' midpoints; guess_ok checks (in double, with a margin far above fp32 rounding) that
+// every crossing lies strictly inside its segment
+template <int N>
+constexpr double guess_h(const float (&bp)[N]) { return ((double)bp[N - 1] - (double)bp[0]) / (N - 1); }
+template <int N>
+constexpr bool guess_ok_uniform(const float (&bp)[N]) {
+  const double h = guess_h(bp), x0 = (double)bp[0] + 0.5 * h;
+  for (int k = 1; k <= N - 3; ++k) {
+    const double b = x0 + k * h;
+    if (!((double)bp[k] + 1e-5 < b && b < (double)bp[k + 1] - 1e-5)) return false;
+  }
+  return true;
+}
+template <int N>
+__device__ __forceinline__ Seg bracket_g_uniform(const float (&bp)[N], const float* pairs, float x) {
+  // (bp is a constexpr table: these fold to literals after inlining)
+  const double h = guess_h(bp);
+  const float ginv = (float)(1.0 / h), c0 = (float)(-((double)bp[0] + 0.5 * h) / h);
+  return bracket_guess<N>(pairs, x, __builtin_fmaf(x, ginv, c0));
+}
+// The union Mach grid {0, .4, .6, .7, .8, .81, .9, 1, 1.1, 1.2, 1.4, 1.6, 1.8} is not uniform:
+// u = 10 x - 4.5, one more past 0.805 (the 0.81 breakpoint), and 5 per unit instead of 10 past
+// 1.2 -- crossings at .55 .65 .75 .805 .85 .95 1.05 1.15 1.3 1.5 (machu_guess_ok checks them)
+__device__ __forceinline__ float machu_u(float x) {
+  x = fminf(x, 4.0f);  // (+inf would make inf - inf below; past 1.8 the guess is the last segment anyway)
+  float u = __builtin_fmaf(x, 10.0f, -4.5f);
+  u += (x > 0.805f) ? 1.0f : 0.0f;
+  return __builtin_fmaf(-5.0f, fmaxf(x - 1.2f, 0.0f), u);
+}
+constexpr bool machu_guess_ok() {
+  // the crossings of machu_u, in double
+  const double b[11] = {0, 0.55, 0.65, 0.75, 0.805, 0.85, 0.95, 1.05, 1.15, 1.3, 1.5};
+  if (sizeof(BP_machu) / sizeof(BP_machu[0]) != 13) return false;
+  for (int k = 1; k <= 10; ++k)
+    if (!((double)BP_machu[k] + 1e-4 < b[k] && b[k] < (double)BP_machu[k + 1] - 1e-4)) return false;
+  return true;
+}
 // uniform grid x0 + k*h (k = 0..N-1): same bracket semantics without a search
 __device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, int n) {
   const float u = (x - x0) * inv_h;
@@ -996,7 +1056,13 @@ struct AeroIn {
   float de, da, dr, dlef, flap, dsb;
 };
 __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6) {
+#ifdef F16_GUESS_BRACKET
+  static_assert(guess_ok_uniform(BP_alpha_bp) && guess_ok_uniform(BP_beta13_bp) && machu_guess_ok(),
+                "guess-bracket crossings must lie inside their segments");
+  const Seg sa = bracket_g_uniform(BP_alpha_bp, T + OFF_pair_alpha, a.alpha);
+#else
   const Seg sa = bracket(BP_alpha_bp, T + OFF_pair_alpha, a.alpha);
+#endif
   // 16 alpha 1-D tables, [12][16 values | 16 alpha-slopes]; FGTable 1-D semantics (clamp
   // at the ends)
   float A[F16_N_A1D];
@@ -1022,7 +1088,11 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     const float d1 = blend(sa.f, p0[2], p0[5]), d2 = blend(sa.f, p1[2], p1[5]);
     ADE[2] = d1 + se.f * (d2 - d1);
   }
+#ifdef F16_GUESS_BRACKET
+  const Seg sb13 = bracket_g_uniform(BP_beta13_bp, T + OFF_pair_beta13, a.beta);
+#else
   const Seg sb13 = bracket(BP_beta13_bp, T + OFF_pair_beta13, a.beta);
+#endif
   float AB13[2];  // Clb, Cnb over (alpha, beta 13)
   {
     const float* p0 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 4;
@@ -1051,7 +1121,11 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     }
   }
   // the nine mach tables on their union breakpoint grid, [13][9 values | 9 mach-slopes]
+#ifdef F16_GUESS_BRACKET
+  const Seg sm = bracket_guess<13>(T + OFF_pair_machu, a.mach, machu_u(a.mach));
+#else
   const Seg sm = bracket(BP_machu, T + OFF_pair_machu, a.mach);
+#endif
   float MU[MACHU_NT];
   {
     const float* r0 = T + OFF_machu_v + (sm.i - 1) * (2 * MACHU_NT);

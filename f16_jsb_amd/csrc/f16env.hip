@@ -657,12 +657,21 @@ struct StepPre {
 // grid of N envs is N/32 waves -- two per SIMD at 65 536 envs -- and the second half of the
 // grid may start `half_delay` cycles late, so that one wave's memory phases (prologue loads,
 // store tail) overlap the other's frames on the same SIMD.
+// XV (windowed plain-step extras, f16_step_winx_kernel / f16env_window_step_ex): XV_FEAT keeps the
+// bound feature histories in the step's epilogue (the rollout-slot build's F16_SLOT_FEATURE_WINDOW
+// code, without the slot); every winx build draws the actions in-kernel when act == NULL
+// (a.sample_act: the f16env_sample_actions stream). The headline instances (XV = 0) carry none of
+// this code.
+enum { XV_X = 1, XV_FEAT = 2 };
 template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false,
-          bool HALF = false>
+          bool HALF = false, int XV = 0>
 __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, float4* sTmpl, int* sDone, float* dynl,
                                           const StepPre* pre = nullptr) {
   const float* sT = GT ? static_cast<const float*>(F16_BLOB_INIT) : sT_lds;
   constexpr bool GUST = (MODE & 2) != 0, DEFER = MODE != 0;
+  // builds that may draw the actions in-kernel (act == NULL): the rollout slot's and the winx
+  constexpr bool SAMPLE = ROLL || (XV & XV_X) != 0;
+  constexpr bool FEATW = ROLL || (XV & XV_FEAT) != 0;  // builds with the feature-window epilogue
   constexpr int EPW = HALF ? 32 : 64;  // envs per wave
 #ifdef F16_STAMPS
   Stamps stamps = {};
@@ -719,16 +728,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     if (pre) {
       const SoA sp = {const_cast<float4*>(pre->sc), pre->n};
       lane_load<GUST>(sp, k, L);
-      if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(pre->act)[k];
+      if (!SAMPLE || !a.sample_act) av = reinterpret_cast<const float4*>(pre->act)[k];
     } else {
       lane_load<GUST>(a.s, k, L);
-      if (!ROLL || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
+      if (!SAMPLE || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   issue_stack_dma();
-  if (ROLL && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
+  if (SAMPLE && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);
   // a lane reset since the last step: the windowed step reads its reset frame (wy[p-1]) now,
   // so the load streams in behind the physics
   // (LDS-DMA into the wave's staging area, [15][64] floats, not registers: nothing stays live
@@ -991,7 +1000,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
         for (int c = 0; c < F16_OBS_DIM; ++c) a.r_next_frame[k * F16_OBS_DIM + c] = fr[c];
       }
     }
-    if (ROLL && a.fwx) {
+    if (FEATW && a.fwx) {
       // the feature window (f16_feature_window_kernel's invariant, written here instead of by a
       // second launch): fx[p] = fy[p] = features of wx[p]; a lane reset now also fills
       // fx[p-K+1 .. p-1] and, ahead of the next step's window fill, fy[p-K+2 .. p-1]. The
@@ -1224,6 +1233,18 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_step_win_nt_kernel(const float
   const StepPre pre = {sc, act, tmpl, n};
   step_body<MODE, false, ROLL, OCC == 2, true, true>(a, sT, sTmpl, sDone, dynl, &pre);
 }
+// the windowed plain step with extras (XV_X | XV_FEAT: the feature window in the epilogue; every
+// winx build takes act == NULL as "draw the actions in-kernel"): f16env_window_step_ex. A kernel
+// of its own, so the headline instances above keep their instruction stream.
+template <int MODE, int OCC, bool NT, int XV>
+__global__ __launch_bounds__(BLOCK, OCC) void f16_step_winx_kernel(const float4* __restrict__ sc,
+                                                                   const float* __restrict__ act,
+                                                                   const float4* __restrict__ tmpl, int64_t n,
+                                                                   StepArgs a) {
+  STEP_SHARED
+  const StepPre pre = {sc, act, tmpl, n};
+  step_body<MODE, false, false, OCC == 2, true, NT, false, XV>(a, sT, sTmpl, sDone, dynl, &pre);
+}
 // the half-populated-wave experiment (HALF above): 256-register build, two waves per SIMD
 template <int MODE>
 __global__ __launch_bounds__(BLOCK, 2) void f16_step_win_half_kernel(const float4* __restrict__ sc,
@@ -1251,6 +1272,22 @@ static WinKernel step_win_kernel_for_r(int mode, int occ, int nt) {
 }
 static WinKernel step_win_kernel_for(int mode, int occ, int nt, bool roll = false) {
   return roll ? step_win_kernel_for_r<true>(mode, occ, nt) : step_win_kernel_for_r<false>(mode, occ, nt);
+}
+template <int XV>
+static WinKernel step_winx_kernel_for_x(int mode, int occ, int nt) {
+  static const WinKernel table[2][2][4] = {
+      {{f16_step_winx_kernel<0, 1, false, XV>, f16_step_winx_kernel<1, 1, false, XV>,
+        f16_step_winx_kernel<2, 1, false, XV>, f16_step_winx_kernel<3, 1, false, XV>},
+       {f16_step_winx_kernel<0, 2, false, XV>, f16_step_winx_kernel<1, 2, false, XV>,
+        f16_step_winx_kernel<2, 2, false, XV>, f16_step_winx_kernel<3, 2, false, XV>}},
+      {{f16_step_winx_kernel<0, 1, true, XV>, f16_step_winx_kernel<1, 1, true, XV>,
+        f16_step_winx_kernel<2, 1, true, XV>, f16_step_winx_kernel<3, 1, true, XV>},
+       {f16_step_winx_kernel<0, 2, true, XV>, f16_step_winx_kernel<1, 2, true, XV>,
+        f16_step_winx_kernel<2, 2, true, XV>, f16_step_winx_kernel<3, 2, true, XV>}}};
+  return table[nt ? 1 : 0][occ == 2 ? 1 : 0][mode & 3];
+}
+static WinKernel step_winx_kernel_for(int mode, int occ, int nt, bool feat) {
+  return feat ? step_winx_kernel_for_x<XV_X | XV_FEAT>(mode, occ, nt) : step_winx_kernel_for_x<XV_X>(mode, occ, nt);
 }
 static constexpr size_t WIN_DYN_LDS = sizeof(float) * (BLOCK / 64) * WIN_WAVE_FLOATS;
 // variant: 0 = LDS tables, 1 wave/SIMD; 1 = LDS tables, 2 waves/SIMD; 2 = global tables.
@@ -2601,9 +2638,10 @@ static int window_check(f16env_t h, const float* hist_cur, const float* hist_oth
 static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,
                             float* hist_cur, float* hist_other, int64_t T, int32_t pos, float* rew,
                             uint8_t* terminated, uint8_t* truncated, double* ep_return, int32_t* ep_len,
-                            int32_t* done_idx, int32_t* n_done) {
+                            int32_t* done_idx, int32_t* n_done, bool ex = false, uint32_t xflags = 0,
+                            uint64_t act_seed = 0, uint64_t act_step = 0) {
   if (!h) return set_err(-1, "null handle");
-  if ((!act && !slot) || !hist_other || !rew || !terminated || !truncated)
+  if ((!act && !slot && !ex) || !hist_other || !rew || !terminated || !truncated)
     return set_err(-1, "act (or a rollout slot)/hist_cur/hist_other/rew/terminated/truncated are required");
   if (int e = window_check(h, hist_cur, hist_other, T, pos)) return e;
   if (hist_cur == hist_other) return set_err(-1, "the two histories must be distinct buffers");
@@ -2637,6 +2675,19 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
       const int b = hist_cur == h->wb.hist[0] ? 0 : 1;
       a.fwx = h->fw[b]; a.fwy = h->fw[b ^ 1];
     }
+  } else if (ex) {  // f16env_window_step_ex: the winx build (in-kernel actions, feature window)
+    a.sample_act = act ? 0 : 1;
+    a.act_seed = act_seed; a.act_step = act_step;
+    if (xflags & ~(uint32_t)F16_STEP_FEATURE_WINDOW) return set_err(-1, "unknown f16env_window_step_ex flags");
+    if (xflags & F16_STEP_FEATURE_WINDOW) {
+      if (!h->fw[0] || !h->fw[1]) return set_err(-1, "F16_STEP_FEATURE_WINDOW: f16env_window_feature_bind first");
+      if (hist_cur != h->wb.hist[0] && hist_cur != h->wb.hist[1])
+        return set_err(-1, "F16_STEP_FEATURE_WINDOW: the step's histories must be the bound ones");
+      if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period <= 0)
+        return set_err(-1, "F16_STEP_FEATURE_WINDOW: not with the deferred-reset step (F16ENV_ICC_PERIOD=0)");
+      const int b = hist_cur == h->wb.hist[0] ? 0 : 1;
+      a.fwx = h->fw[b]; a.fwy = h->fw[b ^ 1];
+    }
   }
   // cfg5 modes: finished lanes are reset inside the step from the reset cache (period 0 or
   // F16ENV_ICC_PERIOD=0: the deferred f16_reset_done_kernel instead)
@@ -2665,9 +2716,10 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
   } else if (int e = done_counter(h, done_idx, a.done_idx, a.n_done, zero_next, st)) {
     return e;
   }
-  WinKernel kern = step_win_kernel_for(h->mode, h->win_occ, h->win_nt, slot != nullptr);
+  WinKernel kern = ex ? step_winx_kernel_for(h->mode, h->win_occ, h->win_nt, a.fwx != nullptr)
+                      : step_win_kernel_for(h->mode, h->win_occ, h->win_nt, slot != nullptr);
   dim3 grid(nblocks(a.E.n));
-  if (h->win_half && !slot) {  // the half-populated-wave experiment: 128 envs per block
+  if (h->win_half && !slot && !ex) {  // the half-populated-wave experiment: 128 envs per block
     static const WinKernel half[4] = {f16_step_win_half_kernel<0>, f16_step_win_half_kernel<1>,
                                       f16_step_win_half_kernel<2>, f16_step_win_half_kernel<3>};
     kern = half[h->mode & 3];
@@ -2738,6 +2790,28 @@ int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t
   const int b = parity & 1;
   return f16env_step_window(h, stream, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew, h->wb.term,
                             h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr);
+}
+
+int f16env_window_step_ex(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos, uint32_t flags,
+                          uint64_t act_seed, uint64_t act_step) {
+  if (!h) return set_err(-1, "null handle");
+  if (!h->wb.hist[0]) return set_err(-1, "f16env_window_bind first");
+  const int b = parity & 1;
+  if (act && !flags)  // nothing extra: the plain windowed step (the headline instance)
+    return f16env_step_window(h, stream, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew, h->wb.term,
+                              h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr);
+  // (rew/terminated/truncated are required by the impl; act may be NULL here)
+  return step_window_impl(h, stream, nullptr, act, h->wb.hist[b], h->wb.hist[b ^ 1], h->wb.T, pos, h->wb.rew,
+                          h->wb.term, h->wb.trunc, h->wb.ep_ret, h->wb.ep_len, nullptr, nullptr, true, flags, act_seed,
+                          act_step);
+}
+
+const char* f16env_window_step_ex_kernel_name(f16env_t h, uint32_t flags) {
+  static thread_local char buf[64];
+  if (!h) return "";
+  snprintf(buf, sizeof buf, "f16_step_winx_kernel<%d, %d, %s, %d>", h->mode & 3, h->win_occ, h->win_nt ? "true" : "false",
+           (flags & F16_STEP_FEATURE_WINDOW) ? (XV_X | XV_FEAT) : XV_X);
+  return buf;
 }
 
 int f16env_window_step_rollout(f16env_t h, void* stream, const f16env_rollout_slot* slot, const float* act,

@@ -22,7 +22,7 @@ import numpy as np
 from . import spaces
 from ._lib import F16EnvError, check, lib
 from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
-                  F16_FLAG_OBS_CHECK, F16_SLOT_CLIP, F16_SLOT_FEATURE_WINDOW,
+                  F16_FLAG_OBS_CHECK, F16_SLOT_CLIP, F16_SLOT_FEATURE_WINDOW, F16_STEP_FEATURE_WINDOW,
                   F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
@@ -59,7 +59,7 @@ class F16Envs:
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
                  autoreset: bool = True, ic=None, nan_guard: bool = False, obs_check: bool = False,
                  obs_layout: str = "contiguous",
-                 history: int = 0, window_order: str = "position", **cfg_kw):
+                 history: int = 0, window_order: str = "position", fused_features: bool = False, **cfg_kw):
         """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
         `history` positions of 64-B frame slots, position-major [T][N][16] (f16env_step_window:
@@ -68,7 +68,12 @@ class F16Envs:
         "env" keeps the histories env-major [N][T][16] instead (strides (T*16, 16, 1)). Both
         layouts give identical values and the same validity (an observation stays valid until
         the step after next). A consumer that needs a flat (N, K*15) array copies the window
-        (reshape); the features kernel (f16_jsb_amd.features) reads it in place."""
+        (reshape); the features kernel (f16_jsb_amd.features) reads it in place.
+        fused_features (windowed layout): every step also keeps the policy features of both
+        windows (obs_features(), features.py:37-67 per frame) in its own epilogue -- the step's
+        feature-window build (f16env_window_step_ex, F16_STEP_FEATURE_WINDOW), no second launch;
+        obs_features() is then a view. Off by default: the plain step's instance carries none of
+        that code."""
         import torch
 
         if not torch.cuda.is_available():
@@ -121,7 +126,10 @@ class F16Envs:
             self._feat_prev_ok = False  # the feature windows hold the last step's ahead fills
             self.feature_window_calls = {"incremental": 0, "full": 0, "fused": 0}
         else:
+            if fused_features:
+                raise ValueError("fused_features needs obs_layout='window'")
             self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
+        self.fused_features = bool(fused_features)
         self._cur = 0
         # rewards (f32), terminated, truncated (u8) in ONE allocation, so a host-side consumer
         # (F16VecEnv's numpy mode) moves the three with a single device-to-host copy
@@ -143,7 +151,10 @@ class F16Envs:
             check(L.f16env_window_bind(self._h, self._hist_ptr[0], self._hist_ptr[1], self.T, *self._win_ptr),
                   "f16env_window_bind")
             self._step_bound = L.f16env_window_step_bound
+            self._step_ex = L.f16env_window_step_ex
             self.terminal_obs = self._window(1)
+            if self.fused_features:
+                self._feature_hist()
         else:
             self._obs_ptr = [o.data_ptr() for o in self._obs]
             self._out_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
@@ -246,15 +257,29 @@ class F16Envs:
                 or tuple(x.shape) != tuple(shape):
             raise ValueError("%s must be a contiguous %s %s tensor on %s" % (name, dtype, tuple(shape), self.device))
 
-    def step(self, actions, done_idx=None, n_done=None, features=None) -> StepOut:
+    def step(self, actions, done_idx=None, n_done=None, features=None, seed=None, step=None) -> StepOut:
         """One env step for all lanes; ``actions`` (N,4) float32 device tensor (or host
         array, copied). Returns device tensors; obs alternates between two buffers.
         done_idx (N,) / n_done (1,) int32 device tensors receive the compacted list of lanes
         that finished (optional). features: an (N, K, 17) float32 device tensor that receives
-        the policy features of the returned obs (features.py:37-67) in the same call."""
+        the policy features of the returned obs (features.py:37-67) in the same call.
+        actions None with seed / step: the actions are drawn inside the step kernel from the
+        sample_actions(seed, step) stream (bit-identical to step(sample_actions(seed, step)),
+        without the sampling launch and the action read; windowed layout: f16env_window_step_ex,
+        contiguous: the rollout-slot step with an empty slot)."""
+        if actions is None:
+            if seed is None or step is None:
+                raise ValueError("actions=None needs seed and step (the in-kernel sample_actions stream)")
+            if done_idx is not None or n_done is not None or features is not None:
+                raise ValueError("in-kernel actions: no done list / features argument")
+            if self.window:
+                return self._step_window_ex(None, int(seed), int(step))
+            return self.step_rollout(seed, step)
         if features is not None:
             return self.step_rollout(0, 0, features=features, policy_actions=actions)
         if self.window:
+            if self.fused_features and done_idx is None and n_done is None:
+                return self._step_window_ex(self._as_act(actions), 0, 0)
             return self._step_window(actions, done_idx, n_done)
         t = self.torch
         if done_idx is None and n_done is None and isinstance(actions, t.Tensor) and actions.device == self.device \
@@ -287,9 +312,8 @@ class F16Envs:
         self._cur ^= 1
         return StepOut(nxt, self.rew, self.term, self.trunc, self.terminal_obs, self.ep_return, self.ep_len)
 
-    def _step_window(self, actions, done_idx, n_done) -> StepOut:
-        """f16env_step_window: the new frame goes to position p+1 of both histories, the
-        observation is the window ending there in the history of the new parity."""
+    def _as_act(self, actions):
+        """actions as an aligned contiguous (N, 4) float32 tensor on the device (copied if not)."""
         t = self.torch
         if isinstance(actions, t.Tensor) and actions.device == self.device and actions.dtype == t.float32 \
                 and actions.is_contiguous() and actions.data_ptr() % 16 == 0:
@@ -299,6 +323,27 @@ class F16Envs:
             act = self._act
         if act.shape != (self.n, 4):
             raise ValueError("actions must be (N, 4), got %s" % (tuple(act.shape),))
+        return act
+
+    def _step_window_ex(self, act, seed: int, step: int) -> StepOut:
+        """f16env_window_step_ex: act None draws the actions in the kernel (sample_actions(seed,
+        step)); a fused_features handle also keeps its feature windows in the step's epilogue
+        whenever they are current before it, and catches them up after a step that could not."""
+        fw = self.fused_features and self._fh is not None and self._feat_prev_ok and self._feat_op == self._op
+        s, cur, p = self._advance()
+        check(self._step_ex(self._h, s, None if act is None else act.data_ptr(), cur, p,
+                            F16_STEP_FEATURE_WINDOW if fw else 0, seed & 0xFFFFFFFFFFFFFFFF,
+                            step & 0xFFFFFFFFFFFFFFFF), "f16env_window_step_ex")
+        out = self._fused_done(fw, self._advanced(cur, p))
+        if self.fused_features and not fw:
+            self.obs_features()  # whole windows + the step's ahead fills: the next step fuses
+        return out
+
+    def _step_window(self, actions, done_idx, n_done) -> StepOut:
+        """f16env_step_window: the new frame goes to position p+1 of both histories, the
+        observation is the window ending there in the history of the new parity."""
+        t = self.torch
+        act = self._as_act(actions)
         if done_idx is not None or n_done is not None:
             if (done_idx is None) != (n_done is None):
                 raise ValueError("done_idx and n_done go together")
@@ -547,15 +592,8 @@ class F16Envs:
         from .features import FEATURES_DIM, features
         if not self.window:
             return features(self.obs)
-        t = self.torch
         n, k, L = self.n, self.k, lib()
-        if self._fh is None:
-            # (positions outside the window are written before they are read)
-            self._fh = t.empty((2, self.T, n, FEATURES_DIM), dtype=t.float32, device=self.device)
-            self._fh_ptr = (self._fh[0].data_ptr(), self._fh[1].data_ptr())
-            # rollout-slot steps update them in their epilogue (F16_SLOT_FEATURE_WINDOW)
-            check(L.f16env_window_feature_bind(self._h, *self._fh_ptr), "f16env_window_feature_bind")
-            self._fviews = [[None] * self.T for _ in range(2)]
+        self._feature_hist()
         cur, p = self._cur, self._p
         if self._feat_op != self._op:
             wrow, wenv = (16, self.T * 16) if self._env_major else (n * 16, 16)
@@ -588,6 +626,18 @@ class F16Envs:
         if v is None:
             v = self._fviews[cur][p] = self._fh[cur, p - k + 1:p + 1].transpose(0, 1)
         return v
+
+    def _feature_hist(self):
+        """The two feature histories [T][N][17] beside the frame histories, allocated and bound
+        once (rollout-slot steps with F16_SLOT_FEATURE_WINDOW and fused_features steps update them
+        in their epilogue); positions outside the window are written before they are read."""
+        if self._fh is None:
+            from .features import FEATURES_DIM
+            t = self.torch
+            self._fh = t.empty((2, self.T, self.n, FEATURES_DIM), dtype=t.float32, device=self.device)
+            self._fh_ptr = (self._fh[0].data_ptr(), self._fh[1].data_ptr())
+            check(lib().f16env_window_feature_bind(self._h, *self._fh_ptr), "f16env_window_feature_bind")
+            self._fviews = [[None] * self.T for _ in range(2)]
 
     def trim(self, ic):
         t = self.torch

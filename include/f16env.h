@@ -49,8 +49,10 @@ extern "C" {
  * f16env_rollout_random has no stack_k / mode limits; new f16env_window_step_rollout,
  * f16env_window_rollout_random, f16env_bootstrap_timeouts, f16env_bootstrap_stash,
  * f16env_bootstrap_apply, f16env_features_window_step, f16env_window_feature_bind
- * (+ F16_SLOT_FEATURE_WINDOW), f16env_abi_version. */
-#define F16ENV_ABI_VERSION 3
+ * (+ F16_SLOT_FEATURE_WINDOW), f16env_abi_version.
+ * 4 (round 5): new f16env_window_step_ex (in-step action draws, F16_STEP_FEATURE_WINDOW) and
+ * f16env_window_step_ex_kernel_name; nothing else changed. */
+#define F16ENV_ABI_VERSION 4
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
 #define F16_OBS_DIM 15
@@ -251,8 +253,27 @@ int f16env_window_bind(f16env_t h, float* hist0, float* hist1, int64_t T, float*
                        uint8_t* truncated, double* ep_return, int32_t* ep_len);
 int f16env_window_step_bound(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos);
 /* The two feature histories ([T][N][17] float32, parity 0 and 1; T as f16env_window_bind) that
- * rollout-slot steps with F16_SLOT_FEATURE_WINDOW update (NULL, NULL: unbind). */
+ * rollout-slot steps with F16_SLOT_FEATURE_WINDOW and f16env_window_step_ex with
+ * F16_STEP_FEATURE_WINDOW update (NULL, NULL: unbind). */
 int f16env_window_feature_bind(f16env_t h, float* feat0, float* feat1);
+/* ABI 4. f16env_window_step_bound with extras, in a kernel instance of its own
+ * (f16_step_winx_kernel; the plain step's instance carries none of this code):
+ *   act == NULL  the actions are drawn in the step from the f16env_sample_actions stream
+ *                (act_seed; env id, act_step): bit-identical to f16env_sample_actions followed by
+ *                f16env_window_step_bound, without the sampling launch or the action read
+ *                (jsbsim_gym.py's action_space.sample() per env, as a device stream);
+ *   flags F16_STEP_FEATURE_WINDOW  the step also brings the feature histories bound by
+ *                f16env_window_feature_bind to its new position (features.py:37-67 of the new
+ *                frame, LMA_features.py:757-765's per-frame transform, written from the frame in
+ *                registers: no second launch), exactly as F16_SLOT_FEATURE_WINDOW does in a
+ *                rollout-slot step; same precondition (both feature windows current before the
+ *                step). Refused with the deferred-reset step (F16ENV_ICC_PERIOD=0).
+ * With act != NULL and flags 0 it is f16env_window_step_bound. */
+#define F16_STEP_FEATURE_WINDOW 0x2
+int f16env_window_step_ex(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos, uint32_t flags,
+                          uint64_t act_seed, uint64_t act_step);
+/* The kernel instance f16env_window_step_ex launches for `flags` (as rocprofv3 demangles it). */
+const char* f16env_window_step_ex_kernel_name(f16env_t h, uint32_t flags);
 /* f16env_reset for windowed observations: K copies of frame 0 into hist_cur's window ending at
  * pos (mask / goals / ic as f16env_reset; jsbsim_gym.py:289-331 x N). */
 int f16env_reset_window(f16env_t h, void* stream, const uint8_t* mask, const float* goals, const double* ic,

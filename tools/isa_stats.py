@@ -52,7 +52,9 @@ def main():
             dump = args[i + 1]
     with tempfile.TemporaryDirectory() as td:
         out = dump or os.path.join(td, "k.s")
+        # the product library's flags (build.py): contraction per source expression, kernarg preload
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize",
+                        "-ffp-contract=on", "-mllvm", "-amdgpu-kernarg-preload-count=8",
                         "-I", os.path.join(ROOT, "include"), "-Wno-unused-value", "-Wno-unused-result",
                         "--cuda-device-only", "-S", SRC, "-o", out, *flags], check=True,
                        stderr=subprocess.DEVNULL)

@@ -99,9 +99,12 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
     }
   } else {
     // LPE lanes per env: lane `sub` writes quarter(s) of the slot: contiguous per wave already
+    // (quarters picked by compile-time indices: a runtime index would put f[] in scratch)
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      for (int j = sub; j < 4; j += LPE) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j % LPE != sub) continue;
         float4* p = reinterpret_cast<float4*>(hist[h] + ((int64_t)pos * n + k) * 16) + j;
         if (NT) __builtin_nontemporal_store(__builtin_bit_cast(v4f, f[j]), reinterpret_cast<v4f*>(p));
         else *p = f[j];
@@ -117,11 +120,11 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
 // ---------------------------------------------------------------------------------------------
 // issue-cost bodies: 16 instructions of one form per iteration, ITER iterations
 typedef float f2 __attribute__((ext_vector_type(2)));
-enum Form { F_FMA, F_FMA_DEP, F_PKFMA, F_PKFMA_DEP, F_PKMUL, F_SUBLIT, F_SIGNCOUNT, F_SALU_MIX, F_EXP, F_MOV, F_N };
+enum Form { F_FMA, F_FMA_DEP, F_PKFMA, F_PKFMA_DEP, F_PKMUL, F_PKADD, F_CNDMASK, F_SUBLIT, F_SIGNCOUNT, F_SALU_MIX, F_EXP, F_MOV, F_N };
 static const char* FORM_NAME[F_N] = {"v_fma_f32 indep", "v_fma_f32 dep", "v_pk_fma_f32 indep", "v_pk_fma_f32 dep",
-                                     "v_pk_mul_f32 indep", "v_sub_f32 literal indep",
+                                     "v_pk_mul_f32 indep", "v_pk_add_f32 indep", "v_cndmask_b32 (vcc) indep", "v_sub_f32 literal indep",
                                      "sign-bit count (v_sub_f32 lit + v_lshrrev + v_add3 per 2)",
-                                     "v_fma_f32 + s_add_u32 alternating", "v_exp_f32 indep", "v_mov_b32 indep"};
+                                     "v_fma_f32 + s_mul_i32 alternating", "v_exp_f32 indep", "v_mov_b32 indep"};
 
 #define R8(X) X X X X X X X X
 template <int FORM>
@@ -150,6 +153,12 @@ __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long lo
     } else if (FORM == F_PKMUL) {
       asm volatile(R8("v_pk_mul_f32 %0, %0, %8\n v_pk_mul_f32 %1, %1, %8\n") : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3),
                    "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pm));
+    } else if (FORM == F_PKADD) {
+      asm volatile(R8("v_pk_add_f32 %0, %0, %8\n v_pk_add_f32 %1, %1, %8\n") : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3),
+                   "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pm));
+    } else if (FORM == F_CNDMASK) {
+      asm volatile(R8("v_cndmask_b32 %0, %0, %1, vcc\n v_cndmask_b32 %1, %1, %0, vcc\n") : "+v"(a0), "+v"(a1)
+                   :: "vcc");
     } else if (FORM == F_SUBLIT) {
       asm volatile(R8("v_sub_f32 %0, 0x3e4ccccd, %0\n v_sub_f32 %1, 0x3f4ccccd, %1\n") : "+v"(a0), "+v"(a1), "+v"(a2),
                    "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
@@ -159,7 +168,8 @@ __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long lo
       asm volatile(R8("v_sub_f32 %2, 0x3e4ccccd, %0\n v_lshrrev_b32 %2, 31, %2\n") : "+v"(a0), "+v"(a1), "+v"(u0),
                    "+v"(u1));
     } else if (FORM == F_SALU_MIX) {
-      asm volatile(R8("v_fma_f32 %0, %0, %3, %4\n s_add_u32 %2, %2, 1\n") : "+v"(a0), "+v"(a1), "+s"(s0)
+      // (s_mul_i32: an SALU op that leaves SCC alone -- s_add_u32 clobbered the loop's branch condition)
+      asm volatile(R8("v_fma_f32 %0, %0, %3, %4\n s_mul_i32 %2, %2, 3\n") : "+v"(a0), "+v"(a1), "+s"(s0)
                    : "v"(m), "v"(b));
     } else if (FORM == F_EXP) {
       asm volatile(R8("v_exp_f32 %0, %0\n v_exp_f32 %1, %1\n") : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4),
@@ -281,6 +291,8 @@ int main(int argc, char** argv) {
     issue_probe<F_PKFMA>(out, cyc, blocks, iters);
     issue_probe<F_PKFMA_DEP>(out, cyc, blocks, iters);
     issue_probe<F_PKMUL>(out, cyc, blocks, iters);
+    issue_probe<F_PKADD>(out, cyc, blocks, iters);
+    issue_probe<F_CNDMASK>(out, cyc, blocks, iters);
     issue_probe<F_SUBLIT>(out, cyc, blocks, iters);
     issue_probe<F_SIGNCOUNT>(out, cyc, blocks, iters);
     issue_probe<F_SALU_MIX>(out, cyc, blocks, iters);
