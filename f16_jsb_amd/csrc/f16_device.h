@@ -467,13 +467,25 @@ constexpr bool machu_guess_ok() {
     if (!((double)BP_machu[k] + 1e-4 < b[k] && b[k] < (double)BP_machu[k + 1] - 1e-4)) return false;
   return true;
 }
-// uniform grid x0 + k*h (k = 0..N-1): same bracket semantics without a search
+// uniform grid x0 + k*h (k = 0..N-1): same bracket semantics without a search. The clamp is
+// done on the float before the floor (v_med3 + v_floor: g = floor(clamp(u, 0, n-2)) equals
+// clamp(floor(u), 0, n-2) for every u), and the factor is u - g: the same segment and factor
+// as flooring to an int first, without the integer min / compare / select and the
+// int-to-float conversion (round 5: 2 x 5 VALU fewer per frame for the engine tables)
+template <bool OLD = false>
 __device__ __forceinline__ Seg bracket_uniform(float x, float x0, float inv_h, int n) {
   const float u = (x - x0) * inv_h;
-  int i = (int)floorf(u) + 1;
-  i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
+  if (OLD) {  // (pre-round-5 form)
+    int i = (int)floorf(u) + 1;
+    i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
+    float f = u - (float)(i - 1);
+    f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
+    return {i, f};
+  }
+  const float g = floorf(__builtin_amdgcn_fmed3f(u, 0.0f, (float)(n - 2)));
+  const int i = (int)g + 1;
   F16_CHECK(i >= 1 && i <= n - 1, DBG_TABLE_SEGMENT);
-  float f = u - (float)(i - 1);
+  float f = u - g;
   f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
   return {i, f};
 }
@@ -481,9 +493,15 @@ __device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (
 
 // atan2 for finite arguments: octant reduction + odd minimax polynomial on [0, 1]
 // (|err| < 1e-7 rad, vs ~40 instructions + special-case handling for OCML atan2f)
+// OLD (the 256-register two-wave builds): IEEE fmaxf / fminf as before round 5, whose code those
+// builds register-allocate without the extra spills the select form cost them
+template <bool OLD = false>
 __device__ __forceinline__ float fatan2(float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
-  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  // (max / min as one compare and two selects, the compare reused for the octant below: IEEE
+  // fmaxf / fminf quiet their |x| operands first, two extra instructions per call)
+  const bool steep = ay > ax;
+  const float mx = OLD ? fmaxf(ax, ay) : (steep ? ay : ax), mn = OLD ? fminf(ax, ay) : (steep ? ax : ay);
   const float a = (mx > 0.0f) ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
   const float s = a * a;
   float p = 2.4566815505e-03f;
@@ -496,7 +514,7 @@ __device__ __forceinline__ float fatan2(float y, float x) {
   p = __builtin_fmaf(p, s, -3.3332596980e-01f);
   p = __builtin_fmaf(p, s, 9.9999988637e-01f);
   float r = a * p;
-  r = (ay > ax) ? 1.57079632679489662f - r : r;
+  r = steep ? 1.57079632679489662f - r : r;
   r = (x < 0.0f) ? 3.14159265358979324f - r : r;
   return copysignf(r, y);
 }
@@ -517,6 +535,14 @@ __device__ __forceinline__ f2v ld2(const float* p) { return f2v{p[0], p[1]}; }
 __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
   return __builtin_elementwise_fma(f2v{f, f}, slope, v);
 }
+// Packed fp32 with explicit VOP3P operand modifiers (round 5): one wave alone issues a
+// v_pk_fma_f32 / v_pk_mul_f32 (two fp32 results, each rounded as the scalar instruction rounds it)
+// at the cost of one v_fma_f32 (profiles/r05_floors.json, issue probe), but the compiler turns
+// mixed-sign or swapped operand pairs into v_mov / v_xor shuffles; these spell the half selects
+// (op_sel: the half of each source feeding the low result, op_sel_hi: the high result) and the
+// per-half negations out. MODS is the modifier string, e.g. "op_sel:[1,1] op_sel_hi:[1,0]".
+#define PK_FMA(d, a, b, c, MODS) asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(d) : "v"(a), "v"(b), "v"(c))
+#define PK_MUL(d, a, b, MODS) asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(d) : "v"(a), "v"(b))
 
 // 1-D lookup: literal breakpoints, LDS (lo, 1/span) pairs, LDS (value, slope) pairs
 template <int N>
@@ -602,7 +628,13 @@ __device__ __forceinline__ Atm atmosphere(float h_ft) {
 // frame latches qc (psf) and the FCS compares it with the qc of each threshold
 // (ModelConsts::qc_vc*, computed in fp64 at create); vc itself (kts) is evaluated from the
 // latch only where it is reported (f16env_get_state).
-__device__ __forceinline__ float impact_pressure(float mach, float p) {
+// (round 5: the subsonic form for every lane and the supersonic one only in waves that hold a
+// supersonic lane -- a wave-uniform branch instead of the exec-mask if / else; the same
+// expressions, so the same values)
+template <bool OLD = false>
+__device__ __forceinline__ float impact_pressure(float mach, float p);
+template <>
+__device__ __forceinline__ float impact_pressure<true>(float mach, float p) {  // (pre-round-5 form)
   if (!(fabsf(mach) > 0.0f)) return 0.0f;
   float pt;
   if (mach < 1.0f) {
@@ -613,6 +645,17 @@ __device__ __forceinline__ float impact_pressure(float mach, float p) {
     pt = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * fsqrt(d));
   }
   return pt - p;
+}
+template <>
+__device__ __forceinline__ float impact_pressure<false>(float mach, float p) {
+  const float x = 1.0f + 0.2f * mach * mach;
+  float pt = p * (x * x * x * fsqrt(x));
+  if (__ballot(mach >= 1.0f) != 0) {  // Rayleigh pitot
+    const float m2 = mach * mach, d = 7.0f * m2 - 1.0f;
+    const float ps = p * 166.92158009316827f * (m2 * m2 * m2 * mach) * rcpf(d * d * fsqrt(d));
+    pt = (mach < 1.0f) ? pt : ps;
+  }
+  return (fabsf(mach) > 0.0f) ? pt - p : 0.0f;
 }
 // calibrated airspeed (kts) from the latched impact pressure
 __device__ __forceinline__ float vcas_from_qc(float qc, const ModelConsts& C) {
@@ -868,9 +911,10 @@ __device__ __forceinline__ void euler(const float* T, float& phi, float& tht, fl
   } else {
     // theta = asin(-T13) as atan2(-T13, cos theta) with cos theta = |(T23, T33)| (Tl2b is a
     // rotation); the polynomial atan2 (|err| < 1e-7 rad) instead of OCML's asinf / atan2f
-    tht = fatan2(-T[2], fsqrt(__builtin_fmaf(T[5], T[5], T[8] * T[8])));
-    phi = fatan2(T[5], T[8]);
-    float p = fatan2(T[1], T[0]);
+    // (once per step, outside the frame loop: the pre-round-5 form, same values)
+    tht = fatan2<true>(-T[2], fsqrt(__builtin_fmaf(T[5], T[5], T[8] * T[8])));
+    phi = fatan2<true>(T[5], T[8]);
+    float p = fatan2<true>(T[1], T[0]);
     if (p < 0.0f) p += 2.0f * PI_F;
     psi = p;
   }
@@ -952,6 +996,7 @@ __device__ __forceinline__ FcsTab fcs_tables(const Lane& L, const float* T) {
 }
 
 // f16.xml:309-984 (document order). T = LDS table blob.
+template <bool OLD = false>
 __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33, float v_fps,
                                         const float* T, const FcsTab& tb, const ModelConsts& C, float dt, bool ic,
                                         FcsOut& o) {
@@ -960,7 +1005,10 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   // Flaps
   // switch (:319-327) as selects of the normalised command (tef_rad * 2.864789)
   const float tef_norm = (qc < C.qc_vc250) ? 0.349f * 2.864789f : ((mach > 0.9f) ? -0.0349f * 2.864789f : 0.0f);
-  L.tef = kin_tef(L.tef, tef_norm, dt, ic);
+  // the flaps sit at their commanded detent almost always (the switch moves only when the
+  // airspeed crosses 250 kts or Mach 0.9): a wave whose every lane is there skips the traverse,
+  // whose result would be its input (kin_tef returns `out` when in == out)
+  if (OLD || ic || __ballot(clipf(tef_norm, -1.0f, 1.0f) != L.tef) != 0) L.tef = kin_tef(L.tef, tef_norm, dt, ic);
   // Roll
   const float roll_err = cmd[0] - L.lx[F16L_P_AERO] * 0.31821f;
   const float roll_pid = pidf(roll_err, L.pri, L.prp, qc < C.qc_vc20, 3.0f, 0.0005f, -0.00125f, dt, ic);
@@ -987,7 +1035,15 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, 2.0f / 0.4f, dt, ic);
   o.dr = aero_scale(L.rud, 0.524f);
   // Leading edge flap (gear pinned up, no WOW)
-  const float lef_rad = (alpha > 0.2618f) ? 0.436f : ((alpha > 0.0873f) ? 0.262f : ((mach > 0.9f) ? -0.0349f : 0.0f));
+  // (as three selects in sequence: the nested conditional compiled to exec-mask branches)
+  float lef_rad;
+  if (OLD) {
+    lef_rad = (alpha > 0.2618f) ? 0.436f : ((alpha > 0.0873f) ? 0.262f : ((mach > 0.9f) ? -0.0349f : 0.0f));
+  } else {
+    lef_rad = (mach > 0.9f) ? -0.0349f : 0.0f;
+    lef_rad = (alpha > 0.0873f) ? 0.262f : lef_rad;
+    lef_rad = (alpha > 0.2618f) ? 0.436f : lef_rad;
+  }
   o.dlef = lef_rad;
   L.lef = kin2(L.lef, lef_rad * 2.293578f, -1.0f, 1.0f, 2.0f / 3.0f, dt, ic);
   // Throttle
@@ -1005,6 +1061,7 @@ __device__ __forceinline__ float seekf(float v, float target, float accel, float
   const float up = fminf(v + dt * accel, target);
   return (v > target) ? dn : ((v < target) ? up : v);
 }
+template <bool OLD = false>
 __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float mach, float h_rho,
                                             float sigma, const float* T, float dt, bool ic) {
   float tp = throttle_pos, aug_cmd = 0.0f;
@@ -1012,9 +1069,9 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   // IdleThrust / MilThrust / AugThrust on one (mach 0..2.6 step 0.2) x (density-alt
   // -10000..60000 step 10000) grid, [14][8][3 values | 3 mach-slopes] (Idle/Mil rows clamped
   // beyond their last mach row, as FGTable does)
-  const Seg er = bracket_uniform(mach, 0.0f, 5.0f, ENGU_NR);
-  const Seg ec = bracket_uniform(h_rho, -10000.0f, 1e-4f, ENGU_NC);
-  const float* e00 = T + OFF_engu_v + ((er.i - 1) * ENGU_NC + ec.i - 1) * 6;
+  const Seg er = bracket_uniform<OLD>(mach, 0.0f, 5.0f, ENGU_NR);
+  const Seg ec = bracket_uniform<OLD>(h_rho, -10000.0f, 1e-4f, ENGU_NC);
+  const float* e00 = T + (OFF_engu_v + __umul24((unsigned)((er.i - 1) * ENGU_NC + ec.i - 1), 6u));
   const float* e01 = e00 + 6;
   float ev[3];
   {
@@ -1067,7 +1124,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   // at the ends)
   float A[F16_N_A1D];
   {
-    const float* r0 = T + OFF_alpha1d + (sa.i - 1) * (2 * F16_N_A1D);
+    const float* r0 = T + (OFF_alpha1d + __umul24((unsigned)(sa.i - 1), 2u * F16_N_A1D));
 #pragma unroll
     for (int k = 0; k < F16_N_A1D / 2; ++k) {
       const f2v r = blend2(sa.f, ld2(r0 + 2 * k), ld2(r0 + F16_N_A1D + 2 * k));
@@ -1080,7 +1137,8 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   const Seg se = bracket(BP_de_bp, T + OFF_pair_de, a.de);
   float ADE[3];  // CDDh, CLDh, CmDh over (alpha, elevator)
   {
-    const float* p0 = T + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 6;
+    // (table offsets as 32-bit 24-bit products: v_mul_u32_u24, not 64-bit multiply-adds)
+    const float* p0 = T + (OFF_ade + __umul24(__umul24((unsigned)(sa.i - 1), F16_N_DE) + (unsigned)(se.i - 1), 6u));
     const float* p1 = p0 + 6;
     const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 3)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 3));
     const f2v r = blend2(se.f, c1, c2 - c1);
@@ -1095,7 +1153,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 #endif
   float AB13[2];  // Clb, Cnb over (alpha, beta 13)
   {
-    const float* p0 = T + OFF_ab13 + ((sa.i - 1) * F16_N_B13 + sb13.i - 1) * 4;
+    const float* p0 = T + (OFF_ab13 + 4u * (__umul24((unsigned)(sa.i - 1), F16_N_B13) + (unsigned)(sb13.i - 1)));
     const float* p1 = p0 + 4;
     const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 2)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 2));
     const f2v r = blend2(sb13.f, c1, c2 - c1);
@@ -1111,7 +1169,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
   }
   float AB7[4];  // Clda, Cldr, Cnda, Cndr over (alpha, beta 7)
   {
-    const float* p0 = T + OFF_ab7 + ((sa.i - 1) * F16_N_B7 + sb7.i - 1) * 8;
+    const float* p0 = T + (OFF_ab7 + 8u * (__umul24((unsigned)(sa.i - 1), F16_N_B7) + (unsigned)(sb7.i - 1)));
     const float* p1 = p0 + 8;
 #pragma unroll
     for (int k = 0; k < 4; k += 2) {
@@ -1128,7 +1186,7 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 #endif
   float MU[MACHU_NT];
   {
-    const float* r0 = T + OFF_machu_v + (sm.i - 1) * (2 * MACHU_NT);
+    const float* r0 = T + (OFF_machu_v + __umul24((unsigned)(sm.i - 1), 2u * MACHU_NT));
 #pragma unroll
     for (int k = 0; k + 1 < MACHU_NT; k += 2) {
       const f2v r = blend2(sm.f, ld2(r0 + k), ld2(r0 + MACHU_NT + k));
@@ -1191,21 +1249,60 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     const float a2 = hx * hx + hy * hy + hz * hz;
     // QExp: cos(a), sin(a)/a; series through a^8 (error < 3e-10 for |a| < 0.5, i.e. body
     // rates below 120 rad/s), exact functions beyond
-    float ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f - a2 * (1.0f / 40320.0f))));
-    float sa = 1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f - a2 * (1.0f / 362880.0f))));
+    // (the same nested FMAs, each level fma(-a2, t, k), written with -a2 as a value so that every
+    // level after the first is one v_fmaak_f32 (a VOP2 form takes the literal; the VOP3 FMA with
+    // a negated operand needs the constant moved into a register first))
+    const float na2 = -a2;
+    float ca, sa;
+    if constexpr (LOWREG) {  // (pre-round-5 form: the same values)
+      ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f - a2 * (1.0f / 40320.0f))));
+      sa = 1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f - a2 * (1.0f / 362880.0f))));
+    } else {
+    ca = __builtin_fmaf(na2, __builtin_fmaf(na2, __builtin_fmaf(na2, __builtin_fmaf(na2, 1.0f / 40320.0f,
+                                                                                         1.0f / 720.0f),
+                                                                       1.0f / 24.0f), 0.5f), 1.0f);
+    sa = __builtin_fmaf(na2, __builtin_fmaf(na2, __builtin_fmaf(na2, __builtin_fmaf(na2, 1.0f / 362880.0f,
+                                                                                   1.0f / 5040.0f),
+                                                                 1.0f / 120.0f), 1.0f / 6.0f), 1.0f);
+    }
     if (__builtin_expect(a2 >= 0.25f, 0)) {
       const float ang = fsqrt(a2);
       ca = cosf(ang);
       sa = sinf(ang) / ang;
     }
     const float p0 = ca, p1 = hx * sa, p2 = hy * sa, p3 = hz * sa;
-    const float q0 = L.q[0], q1 = L.q[1], q2 = L.q[2], q3 = L.q[3];
-    float n0 = q0 * p0 - q1 * p1 - q2 * p2 - q3 * p3;
-    float n1 = q0 * p1 + q1 * p0 + q2 * p3 - q3 * p2;
-    float n2 = q0 * p2 - q1 * p3 + q2 * p0 + q3 * p1;
-    float n3 = q0 * p3 + q1 * p2 - q2 * p1 + q3 * p0;
+    // n = q (x) p, as the scalar statement
+    //   n0 = q0 p0 - q1 p1 - q2 p2 - q3 p3      n1 = q0 p1 + q1 p0 + q2 p3 - q3 p2
+    //   n2 = q0 p2 - q1 p3 + q2 p0 + q3 p1      n3 = q0 p3 + q1 p2 - q2 p1 + q3 p0
+    // (fp-contract=on: a product, then three FMAs in that order) in packed pairs (n0, n1),
+    // (n2, n3): per half the same product and FMAs, so the same roundings, in 8 instructions
+    // instead of 16 (the operand halves and signs by VOP3P modifiers, PK_FMA)
+    // (the 256-register two-waves-per-SIMD builds keep the scalar form: the packed operands'
+    // aligned register pairs pushed cfg5's <3, 2> build from 12 to 32 B of scratch)
+    if constexpr (LOWREG) {
+      const float q0 = L.q[0], q1 = L.q[1], q2 = L.q[2], q3 = L.q[3];
+      const float n0 = q0 * p0 - q1 * p1 - q2 * p2 - q3 * p3;
+      const float n1 = q0 * p1 + q1 * p0 + q2 * p3 - q3 * p2;
+      const float n2 = q0 * p2 - q1 * p3 + q2 * p0 + q3 * p1;
+      const float n3 = q0 * p3 + q1 * p2 - q2 * p1 + q3 * p0;
+      const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);  // |n| ~ 1
+      L.q[0] = n0 * rn; L.q[1] = n1 * rn; L.q[2] = n2 * rn; L.q[3] = n3 * rn;
+    } else {
+    const f2v Q01 = {L.q[0], L.q[1]}, Q23 = {L.q[2], L.q[3]}, P01 = {p0, p1}, P23 = {p2, p3};
+    f2v m, N01, N23;
+    PK_MUL(m, Q01, P01, "op_sel:[1,1] op_sel_hi:[1,0]");                                 // q1 (p1, p0)
+    PK_FMA(N01, Q01, P01, m, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,1]");         // + q0 (p0, p1)
+    PK_FMA(N01, Q23, P23, N01, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]");       // + q2 (-p2, p3)
+    PK_FMA(N01, Q23, P23, N01, "op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]");  // + q3 (-p3, -p2)
+    PK_MUL(m, Q01, P23, "op_sel:[1,1] op_sel_hi:[1,0]");                                 // q1 (p3, p2)
+    PK_FMA(N23, Q01, P23, m, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,1]");         // + q0 (p2, p3)
+    PK_FMA(N23, Q23, P01, N23, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]");       // + q2 (p0, -p1)
+    PK_FMA(N23, Q23, P01, N23, "op_sel:[1,1,0] op_sel_hi:[1,0,1]");                      // + q3 (p1, p0)
+    const float n0 = N01.x, n1 = N01.y, n2 = N23.x, n3 = N23.y;
     const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);  // |n| ~ 1
-    L.q[0] = n0 * rn; L.q[1] = n1 * rn; L.q[2] = n2 * rn; L.q[3] = n3 * rn;
+    const f2v R = {rn, rn}, QN01 = N01 * R, QN23 = N23 * R;
+    L.q[0] = QN01.x; L.q[1] = QN01.y; L.q[2] = QN23.x; L.q[3] = QN23.y;
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) L.wI[j] += dt * L.wId[j];
     // AB3 position: r += dt/12 (23 v0 - 16 v1 + 5 v2) = dt v0 + dt/12 (-16 dv1 + 5 dv2)
@@ -1238,9 +1335,9 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   const bool moving = muw > 0.0f;
   // JSBSim's alpha = beta = 0 when not moving, as fatan2(+0, 0) = +0 on guarded inputs:
   // straight-line code instead of two divergent branches around the polynomials
-  const float alpha = fatan2(moving ? wa : 0.0f, ua);
+  const float alpha = fatan2<LOWREG>(moving ? wa : 0.0f, ua);
   const float suw = fsqrt(muw);
-  const float beta = fatan2(moving ? va : 0.0f, suw);
+  const float beta = fatan2<LOWREG>(moving ? va : 0.0f, suw);
   const float iuw = rcpf(suw), ivt = rcpf(vt);
   const float ca_ = moving ? ua * iuw : 1.0f, sa_ = moving ? wa * iuw : 0.0f;
   const float cb_ = moving ? suw * ivt : 1.0f, sb_ = moving ? va * ivt : 0.0f;
@@ -1269,10 +1366,10 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   F16_STAMP(stamps, ST_ATM);
   // -- Systems (reads the previous frame's latch) --
   FcsOut fc;
-  fcs_run(L, cmd, d.Tl2b[8], d.uvw[1], T, tb, C, dt, ic, fc);
+  fcs_run<LOWREG>(L, cmd, d.Tl2b[8], d.uvw[1], T, tb, C, dt, ic, fc);
   F16_STAMP(stamps, ST_FCS);
   // -- Propulsion --
-  const float thrust = engine_run(L, fc.throttle, mach, h, sigma, T, dt, ic);
+  const float thrust = engine_run<LOWREG>(L, fc.throttle, mach, h, sigma, T, dt, ic);
   F16_STAMP(stamps, ST_ENGINE);
   // -- Aerodynamics --
   AeroIn ai;
@@ -1316,7 +1413,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   // -- Auxiliary latch for the next frame's FCS --
   if (LOWREG) __builtin_amdgcn_sched_barrier(0);
   L.lx[F16L_ALPHA] = alpha; L.lx[F16L_BETA] = beta; L.lx[F16L_MACH] = mach;
-  L.lx[F16L_VC_KTS] = impact_pressure(mach, atm.P); L.lx[F16L_VG_FPS] = vg;
+  L.lx[F16L_VC_KTS] = impact_pressure<LOWREG>(mach, atm.P); L.lx[F16L_VG_FPS] = vg;
   L.lx[F16L_P_AERO] = d.pqr[0]; L.lx[F16L_Q_AERO] = d.pqr[1]; L.lx[F16L_R_AERO] = d.pqr[2];
   L.lx[F16L_NPY] = npy; L.lx[F16L_NPZ] = npz;
   F16_STAMP(stamps, ST_ACCEL);

@@ -72,6 +72,8 @@ for s in $STEPS; do
     floors)  # empty / copy / issue-cost floors, then the step's own (ds 4 / 0 / 1 / 2)
       run floors_$TAG 120 tools/probes/floors 65536 300
       run floors_step_$TAG 300 python tools/floors_step.py --json "$OUT/floors_step_$TAG.json" ;;
+    ab)  # same-box A/B of f16_jsb_amd/libf16env_ab_*.so against the product: bit identity + kernel time
+      run ab_$TAG 900 python tools/ab_builds.py run --rounds ${AB_ROUNDS:-2} --json "$OUT/ab_$TAG.json" ;;
     launch2)  # bench.py --gpus 2 with no external launcher (gloo: 2 ranks share the box's GPU)
       run bench_launch2_$TAG 600 python bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
     iccsweep)  # cfg5 reset-cache refill period, same box

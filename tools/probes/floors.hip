@@ -120,13 +120,21 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
 // ---------------------------------------------------------------------------------------------
 // issue-cost bodies: 16 instructions of one form per iteration, ITER iterations
 typedef float f2 __attribute__((ext_vector_type(2)));
-enum Form { F_FMA, F_FMA_DEP, F_PKFMA, F_PKFMA_DEP, F_PKMUL, F_PKADD, F_CNDMASK, F_SUBLIT, F_SIGNCOUNT, F_SALU_MIX, F_EXP, F_MOV, F_N };
-static const char* FORM_NAME[F_N] = {"v_fma_f32 indep", "v_fma_f32 dep", "v_pk_fma_f32 indep", "v_pk_fma_f32 dep",
-                                     "v_pk_mul_f32 indep", "v_pk_add_f32 indep", "v_cndmask_b32 (vcc) indep", "v_sub_f32 literal indep",
+enum Form { F_FMA, F_FMA_DEP, F_PKFMA, F_PKFMA_DEP, F_PKMUL, F_PKADD, F_CNDMASK, F_CNDMASK_INDEP, F_CNDMASK_SGPR, F_CMP, F_MED3, F_MAX, F_CNDMASK_MIX, F_FMA64, F_MULLO, F_MUL24, F_CVT64, F_SUBLIT, F_SIGNCOUNT, F_SALU_MIX, F_EXP, F_MOV, F_N };
+static const char* FORM_NAME[F_N] = {"v_fma_f32 8 chains", "v_fma_f32 dep", "v_pk_fma_f32 8 chains", "v_pk_fma_f32 dep",
+                                     "v_pk_mul_f32 indep", "v_pk_add_f32 indep", "v_cndmask_b32 (vcc) dependent pairs",
+                                     "v_cndmask_b32 (vcc) 8 chains", "v_cndmask_b32_e64 (sgpr pair mask) 8 chains",
+                                     "v_cmp_gt_f32 (vcc) indep", "v_med3_f32 8 chains", "v_max_f32 8 chains",
+                                     "v_cndmask_b32 (vcc) 1 per 3 fma", "v_fma_f64 indep", "v_mul_lo_u32 indep", "v_mul_u32_u24 indep",
+                                     "v_cvt_f64_f32 indep", "v_sub_f32 literal indep",
                                      "sign-bit count (v_sub_f32 lit + v_lshrrev + v_add3 per 2)",
                                      "v_fma_f32 + s_mul_i32 alternating", "v_exp_f32 indep", "v_mov_b32 indep"};
 
 #define R8(X) X X X X X X X X
+// 8 independent chains: the same instruction on %0 .. %7, twice (16 instructions)
+#define C8(OP, TAIL) OP " %0, %0" TAIL "\n" OP " %1, %1" TAIL "\n" OP " %2, %2" TAIL "\n" OP " %3, %3" TAIL "\n" \
+                     OP " %4, %4" TAIL "\n" OP " %5, %5" TAIL "\n" OP " %6, %6" TAIL "\n" OP " %7, %7" TAIL "\n"
+#define C16(OP, TAIL) C8(OP, TAIL) C8(OP, TAIL)
 template <int FORM>
 __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long long* cyc, int iters, float seed) {
   float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
@@ -135,18 +143,19 @@ __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long lo
      p7 = p3 + 1.f;
   const float m = 0.999f, b = 1e-3f;
   const f2 pm = {m, m}, pb = {b, b};
-  uint32_t u0 = 0, u1 = 0;
+  uint32_t u0 = threadIdx.x, u1 = u0 + 3, u2 = 5;
+  double d0 = a0, d1 = a1, d2 = a2, d3 = a3, dm = 0.999;
   uint32_t s0 = 0;
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
     if (FORM == F_FMA) {
-      asm volatile(R8("v_fma_f32 %0, %0, %8, %9\n v_fma_f32 %1, %1, %8, %9\n") : "+v"(a0), "+v"(a1), "+v"(a2),
+      asm volatile(C16("v_fma_f32", ", %8, %9") : "+v"(a0), "+v"(a1), "+v"(a2),
                    "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m), "v"(b));
     } else if (FORM == F_FMA_DEP) {
       asm volatile(R8("v_fma_f32 %0, %0, %1, %2\n v_fma_f32 %0, %0, %1, %2\n") : "+v"(a0) : "v"(m), "v"(b));
     } else if (FORM == F_PKFMA) {
-      asm volatile(R8("v_pk_fma_f32 %0, %0, %8, %9\n v_pk_fma_f32 %1, %1, %8, %9\n") : "+v"(p0), "+v"(p1), "+v"(p2),
+      asm volatile(C16("v_pk_fma_f32", ", %8, %9") : "+v"(p0), "+v"(p1), "+v"(p2),
                    "+v"(p3), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pm), "v"(pb));
     } else if (FORM == F_PKFMA_DEP) {
       asm volatile(R8("v_pk_fma_f32 %0, %0, %1, %2\n v_pk_fma_f32 %0, %0, %1, %2\n") : "+v"(p0) : "v"(pm), "v"(pb));
@@ -159,6 +168,33 @@ __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long lo
     } else if (FORM == F_CNDMASK) {
       asm volatile(R8("v_cndmask_b32 %0, %0, %1, vcc\n v_cndmask_b32 %1, %1, %0, vcc\n") : "+v"(a0), "+v"(a1)
                    :: "vcc");
+    } else if (FORM == F_CNDMASK_INDEP) {
+      asm volatile(C16("v_cndmask_b32", ", %8, vcc") : "+v"(a0), "+v"(a1), "+v"(a2),
+                   "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m) : "vcc");
+    } else if (FORM == F_CNDMASK_SGPR) {
+      asm volatile("s_mov_b64 s[40:41], exec\n" C16("v_cndmask_b32_e64", ", %8, s[40:41]")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m) : "s40", "s41");
+    } else if (FORM == F_CMP) {
+      asm volatile(R8("v_cmp_gt_f32 vcc, %0, %2\n v_cmp_gt_f32 vcc, %1, %2\n") : "+v"(a0), "+v"(a1) : "v"(m) : "vcc");
+    } else if (FORM == F_MED3) {
+      asm volatile(C16("v_med3_f32", ", %8, %9") : "+v"(a0), "+v"(a1), "+v"(a2),
+                   "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m), "v"(b));
+    } else if (FORM == F_MAX) {
+      asm volatile(C16("v_max_f32", ", %8") : "+v"(a0), "+v"(a1), "+v"(a2),
+                   "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m));
+    } else if (FORM == F_CNDMASK_MIX) {
+      // 4 groups of (3 independent FMAs + 1 select): 16 instructions
+      asm volatile("v_cmp_gt_f32 vcc, %8, %9\n" R8("v_fma_f32 %0, %0, %8, %9\n v_cndmask_b32 %1, %1, %8, vcc\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(m), "v"(b) : "vcc");
+    } else if (FORM == F_FMA64) {
+      asm volatile(R8("v_fma_f64 %0, %0, %4, %4\n v_fma_f64 %1, %1, %4, %4\n") : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)
+                   : "v"(dm));
+    } else if (FORM == F_MULLO) {
+      asm volatile(R8("v_mul_lo_u32 %0, %0, %2\n v_mul_lo_u32 %1, %1, %2\n") : "+v"(u0), "+v"(u1) : "v"(u2));
+    } else if (FORM == F_MUL24) {
+      asm volatile(R8("v_mul_u32_u24 %0, %0, %2\n v_mul_u32_u24 %1, %1, %2\n") : "+v"(u0), "+v"(u1) : "v"(u2));
+    } else if (FORM == F_CVT64) {
+      asm volatile(R8("v_cvt_f64_f32 %0, %2\n v_cvt_f64_f32 %1, %3\n") : "=v"(d0), "=v"(d1) : "v"(a0), "v"(a1));
     } else if (FORM == F_SUBLIT) {
       asm volatile(R8("v_sub_f32 %0, 0x3e4ccccd, %0\n v_sub_f32 %1, 0x3f4ccccd, %1\n") : "+v"(a0), "+v"(a1), "+v"(a2),
                    "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
@@ -182,7 +218,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_issue(float* out, unsigned long lo
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   const float r = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + p0.x + p1.y + p2.x + p3.y + p4.x + p5.y + p6.x + p7.y +
-                  (float)(u0 + u1 + s0);
+                  (float)(u0 + u1 + s0) + (float)(d0 + d1 + d2 + d3);
   const int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   out[g] = r;
   if ((threadIdx.x & 63) == 0) cyc[g >> 6] = t1 - t0;  // a vector store from lane 0
@@ -285,7 +321,7 @@ int main(int argc, char** argv) {
   copy_line("copy_plain_1wave", 1, k_copy<1, false>);
   copy_line("copy_plain_4wave", 4, k_copy<4, false>);
   const int iters = 256;
-  for (int blocks : {256, 1024}) {
+  for (int blocks : {256}) {
     issue_probe<F_FMA>(out, cyc, blocks, iters);
     issue_probe<F_FMA_DEP>(out, cyc, blocks, iters);
     issue_probe<F_PKFMA>(out, cyc, blocks, iters);
@@ -293,6 +329,16 @@ int main(int argc, char** argv) {
     issue_probe<F_PKMUL>(out, cyc, blocks, iters);
     issue_probe<F_PKADD>(out, cyc, blocks, iters);
     issue_probe<F_CNDMASK>(out, cyc, blocks, iters);
+    issue_probe<F_CNDMASK_INDEP>(out, cyc, blocks, iters);
+    issue_probe<F_CNDMASK_SGPR>(out, cyc, blocks, iters);
+    issue_probe<F_CMP>(out, cyc, blocks, iters);
+    issue_probe<F_MED3>(out, cyc, blocks, iters);
+    issue_probe<F_MAX>(out, cyc, blocks, iters);
+    issue_probe<F_CNDMASK_MIX>(out, cyc, blocks, iters);
+    issue_probe<F_FMA64>(out, cyc, blocks, iters);
+    issue_probe<F_MULLO>(out, cyc, blocks, iters);
+    issue_probe<F_MUL24>(out, cyc, blocks, iters);
+    issue_probe<F_CVT64>(out, cyc, blocks, iters);
     issue_probe<F_SUBLIT>(out, cyc, blocks, iters);
     issue_probe<F_SIGNCOUNT>(out, cyc, blocks, iters);
     issue_probe<F_SALU_MIX>(out, cyc, blocks, iters);
