@@ -91,6 +91,14 @@ struct ModelConsts {
   float qc_vc250, qc_vc20, qc_vc10, qc_vc5;  // impact pressure (psf) at these calibrated airspeeds (kts)
   double cos_dE, sin_dE;     // rotation of the Earth per frame (omega * dt)
   double dt;
+  double epa_dt;             // OMEGA_E * dt: the Earth angle's advance per frame
+  // the frame's fp32 products of dt with constants, formed once on the host (build_consts: the
+  // same fp32 multiplications the frames did per frame, so the same values) and read as
+  // wave-uniform kernel arguments: dt, dt / 2, dt / 12; the kinematic actuators' per-frame travel
+  // (rate * dt); the PID integrators' ki * dt
+  float dt_f, half_dt, dt_12;
+  float lim_ail, lim_rud, lim_lef, lim_sb;
+  float kidt_roll, kidt_pitch, kidt_yaw;
 };
 
 // Mass properties (FGMassBalance with the tanks pinned to 1000 lb before every run(),
@@ -495,9 +503,11 @@ __device__ __forceinline__ float lerp1(float f, float a, float b) { return f * (
 // (|err| < 1e-7 rad, vs ~40 instructions + special-case handling for OCML atan2f)
 // OLD (the 256-register two-wave builds): IEEE fmaxf / fminf as before round 5, whose code those
 // builds register-allocate without the extra spills the select form cost them
-template <bool OLD = false>
+// XPOS: x is known to be +0 or positive (a square root): |x| = x and the x < 0 half-turn never
+// applies (the same values, three instructions fewer)
+template <bool OLD = false, bool XPOS = false>
 __device__ __forceinline__ float fatan2(float y, float x) {
-  const float ax = fabsf(x), ay = fabsf(y);
+  const float ax = XPOS ? x : fabsf(x), ay = fabsf(y);
   // (max / min as one compare and two selects, the compare reused for the octant below: IEEE
   // fmaxf / fminf quiet their |x| operands first, two extra instructions per call)
   const bool steep = ay > ax;
@@ -515,7 +525,7 @@ __device__ __forceinline__ float fatan2(float y, float x) {
   p = __builtin_fmaf(p, s, 9.9999988637e-01f);
   float r = a * p;
   r = steep ? 1.57079632679489662f - r : r;
-  r = (x < 0.0f) ? 3.14159265358979324f - r : r;
+  if (!XPOS) r = (x < 0.0f) ? 3.14159265358979324f - r : r;
   return copysignf(r, y);
 }
 
@@ -531,7 +541,12 @@ __device__ __forceinline__ float blend(float f, float v, float slope) { return _
 // the same on two tables at once (v_pk_fma_f32: two fp32 FMAs per lane per instruction, the
 // factor broadcast by op_sel); values/slopes come from LDS as register pairs
 typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v ld2(const float* p) { return f2v{p[0], p[1]}; }
+// (p at an even float offset -- every pair the blob stores for a packed blend, tools/gen_tables.py
+// -- read as one aligned 8-byte element, so the pair lands in an aligned register pair)
+__device__ __forceinline__ f2v ld2(const float* p) {
+  const float2 v = *reinterpret_cast<const float2*>(p);
+  return f2v{v.x, v.y};
+}
 __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
   return __builtin_elementwise_fma(f2v{f, f}, slope, v);
 }
@@ -933,11 +948,10 @@ __device__ __forceinline__ bool eq_roundoff(float a, float b) {
 // FGKinematic's "already there within round-off" test (oracle eq_roundoff, fp64) is not
 // restated in fp32: it would hold the output up to 2 fp32 ulps short of the input where the
 // oracle moves it onto the input. Branch-free.
-__device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float rate, float dt,
-                                      bool ic) {
+// lim = dt * rate (ModelConsts lim_*)
+__device__ __forceinline__ float kin2(float out, float in, float d0, float d1, float lim, bool ic) {
   in = clipf(in, d0, d1);
   if (ic) return in;  // compile-time after inlining
-  const float lim = dt * rate;
   return out + clipf(in - out, -lim, lim);
 }
 // TEF kinematic: detents {-1, 0, 1}, times {3, 0, 3} (f16.xml:334-350), the FGKinematic
@@ -963,10 +977,11 @@ __device__ __forceinline__ float kin_tef(float out, float in, float dt, bool ic)
 // (f16.xml:383-389, :594-604, :716-727): trigger 0 integrates, 1 holds, and the reset branch
 // (trigger < 0) cannot occur, so the trigger is passed as `integrate` (trigger == 0). KD: the
 // g-load PID has kd = 0 (no derivative term; its previous input is still tracked).
+// kidt = ki * dt (ModelConsts kidt_*)
 template <bool KD = true>
 __device__ __forceinline__ float pidf(float in, float& itot, float& prev, bool integrate, float kp,
-                                      float ki, float kd, float dt, bool ic) {
-  if (!ic && integrate) itot += ki * dt * in;
+                                      float kidt, float kd, float dt, bool ic) {
+  if (!ic && integrate) itot += kidt * in;
   float out = kp * in + itot;
   if (KD) out += kd * (ic ? 0.0f : (in - prev) * rcpf(dt));
   prev = in;
@@ -1011,10 +1026,10 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   if (OLD || ic || __ballot(clipf(tef_norm, -1.0f, 1.0f) != L.tef) != 0) L.tef = kin_tef(L.tef, tef_norm, dt, ic);
   // Roll
   const float roll_err = cmd[0] - L.lx[F16L_P_AERO] * 0.31821f;
-  const float roll_pid = pidf(roll_err, L.pri, L.prp, qc < C.qc_vc20, 3.0f, 0.0005f, -0.00125f, dt, ic);
+  const float roll_pid = pidf(roll_err, L.pri, L.prp, qc < C.qc_vc20, 3.0f, C.kidt_roll, -0.00125f, dt, ic);
   const float roll_cmd = clipf(roll_pid + cmd[0], -1.0f, 1.0f);
   o.da = aero_scale(roll_cmd, 0.375f);
-  L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
+  L.ail = kin2(L.ail, roll_cmd, -1.0f, 1.0f, C.lim_ail, ic);
   const float asc = L.ail * tb.asc;
   const float lflap = clipf(-L.tef - asc, -1.0f, 1.0f);
   const float rflap = clipf(L.tef - asc, -1.0f, 1.0f);
@@ -1024,15 +1039,15 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
   const float ele_lim = clipf(cmd[1], -1.0f, 0.44f);
   const float ele_sched = ele_lim * tb.ele;
   const float pitch_err = ele_sched + L.lx[F16L_Q_AERO] * 6.2f - g_corr * 0.020f;
-  const float gpid = clipf(pidf<false>(pitch_err, L.ppi, L.ppp, qc < C.qc_vc5, 0.3f, 0.025f, 0.0f, dt, ic), -1.0f, 1.0f);
+  const float gpid = clipf(pidf<false>(pitch_err, L.ppi, L.ppp, qc < C.qc_vc5, 0.3f, C.kidt_pitch, 0.0f, dt, ic), -1.0f, 1.0f);
   const float pitch_sched = clipf(ele_sched + alpha * 1.0472f + gpid, -1.0f, 1.0f);
-  L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, 2.0f / 0.3f, dt, ic);
+  L.ele = kin2(L.ele, pitch_sched, -1.0f, 1.0f, C.lim_ail, ic);  // (the same 2 / 0.3 s rate)
   o.de = aero_scale(L.ele, 0.436f);
   // Yaw
   const float yaw_err = cmd[2] + L.lx[F16L_R_AERO] * tb.yaw + L.lx[F16L_NPY] * 0.25f;
-  const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, qc < C.qc_vc10, 0.1055f, 0.00001f, 0.00005f, dt, ic), -1.0f, 1.0f);
+  const float ypid = clipf(pidf(yaw_err, L.pyi, L.pyp, qc < C.qc_vc10, 0.1055f, C.kidt_yaw, 0.00005f, dt, ic), -1.0f, 1.0f);
   const float yaw_sched = clipf(cmd[2] + ypid, -1.0f, 1.0f);
-  L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, 2.0f / 0.4f, dt, ic);
+  L.rud = kin2(L.rud, yaw_sched, -1.0f, 1.0f, C.lim_rud, ic);
   o.dr = aero_scale(L.rud, 0.524f);
   // Leading edge flap (gear pinned up, no WOW)
   // (as three selects in sequence: the nested conditional compiled to exec-mask branches)
@@ -1045,13 +1060,13 @@ __device__ __forceinline__ void fcs_run(Lane& L, const float* cmd, float tl2b_33
     lef_rad = (alpha > 0.2618f) ? 0.436f : lef_rad;
   }
   o.dlef = lef_rad;
-  L.lef = kin2(L.lef, lef_rad * 2.293578f, -1.0f, 1.0f, 2.0f / 3.0f, dt, ic);
+  L.lef = kin2(L.lef, lef_rad * 2.293578f, -1.0f, 1.0f, C.lim_lef, ic);
   // Throttle
   o.throttle = cmd[3] * 2.0f;
   // Speedbrake
   const float sb_init = (alpha * RAD2DEG_F >= 53.0f && v_fps <= 18.0f) ? 1.0f : 0.0f;
   const float sb_sched = sb_init * T[OFF_fcs_vd_speedbrake_scheduler];  // gear-cmd-norm = 0
-  L.sb = kin2(L.sb, sb_sched * 60.0f, 0.0f, 60.0f, 60.0f, dt, ic);
+  L.sb = kin2(L.sb, sb_sched * 60.0f, 0.0f, 60.0f, C.lim_sb, ic);
   o.dsb = L.sb * (1.0f / RAD2DEG_F);
 }
 
@@ -1067,18 +1082,19 @@ __device__ __forceinline__ float engine_run(Lane& L, float throttle_pos, float m
   float tp = throttle_pos, aug_cmd = 0.0f;
   if (tp > 1.0f) { aug_cmd = tp - 1.0f; tp -= aug_cmd; }
   // IdleThrust / MilThrust / AugThrust on one (mach 0..2.6 step 0.2) x (density-alt
-  // -10000..60000 step 10000) grid, [14][8][3 values | 3 mach-slopes] (Idle/Mil rows clamped
-  // beyond their last mach row, as FGTable does)
+  // -10000..60000 step 10000) grid, [14][8][2 values | 2 mach-slopes | value | mach-slope]
+  // (Idle/Mil rows clamped beyond their last mach row, as FGTable does)
   const Seg er = bracket_uniform<OLD>(mach, 0.0f, 5.0f, ENGU_NR);
   const Seg ec = bracket_uniform<OLD>(h_rho, -10000.0f, 1e-4f, ENGU_NC);
   const float* e00 = T + (OFF_engu_v + __umul24((unsigned)((er.i - 1) * ENGU_NC + ec.i - 1), 6u));
   const float* e01 = e00 + 6;
   float ev[3];
   {
-    const f2v c1 = blend2(er.f, ld2(e00), ld2(e00 + 3)), c2 = blend2(er.f, ld2(e01), ld2(e01 + 3));
+    const f2v c1 = blend2(er.f, ld2(e00), ld2(e00 + 2)), c2 = blend2(er.f, ld2(e01), ld2(e01 + 2));
     const f2v r = blend2(ec.f, c1, c2 - c1);
     ev[0] = r.x; ev[1] = r.y;
-    const float d1 = blend(er.f, e00[2], e00[5]), d2 = blend(er.f, e01[2], e01[5]);
+    const f2v t1 = ld2(e00 + 4), t2 = ld2(e01 + 4);
+    const float d1 = blend(er.f, t1.x, t1.y), d2 = blend(er.f, t2.x, t2.y);
     ev[2] = d1 + ec.f * (d2 - d1);
   }
   const float idle = 17800.0f * ev[0];
@@ -1132,7 +1148,8 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
       A[2 * k + 1] = r.y;
     }
   }
-  // 2-D over (alpha, X), entries [12][X][G values | G alpha-slopes]: blend along alpha at the
+  // 2-D over (alpha, X), entries [12][X][G values | G alpha-slopes] (the three (alpha, elevator)
+  // tables pairwise: [2 values | 2 alpha-slopes | value | alpha-slope]): blend along alpha at the
   // two bracketing X columns, then along X
   const Seg se = bracket(BP_de_bp, T + OFF_pair_de, a.de);
   float ADE[3];  // CDDh, CLDh, CmDh over (alpha, elevator)
@@ -1140,10 +1157,11 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     // (table offsets as 32-bit 24-bit products: v_mul_u32_u24, not 64-bit multiply-adds)
     const float* p0 = T + (OFF_ade + __umul24(__umul24((unsigned)(sa.i - 1), F16_N_DE) + (unsigned)(se.i - 1), 6u));
     const float* p1 = p0 + 6;
-    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 3)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 3));
+    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 2)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 2));
     const f2v r = blend2(se.f, c1, c2 - c1);
     ADE[0] = r.x; ADE[1] = r.y;
-    const float d1 = blend(sa.f, p0[2], p0[5]), d2 = blend(sa.f, p1[2], p1[5]);
+    const f2v t1 = ld2(p0 + 4), t2 = ld2(p1 + 4);
+    const float d1 = blend(sa.f, t1.x, t1.y), d2 = blend(sa.f, t2.x, t2.y);
     ADE[2] = d1 + se.f * (d2 - d1);
   }
 #ifdef F16_GUESS_BRACKET
@@ -1178,7 +1196,8 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
       AB7[k] = r.x; AB7[k + 1] = r.y;
     }
   }
-  // the nine mach tables on their union breakpoint grid, [13][9 values | 9 mach-slopes]
+  // the nine mach tables on their union breakpoint grid, [13][(2 values | 2 mach-slopes) x 4 |
+  // value | mach-slope]
 #ifdef F16_GUESS_BRACKET
   const Seg sm = bracket_guess<13>(T + OFF_pair_machu, a.mach, machu_u(a.mach));
 #else
@@ -1189,10 +1208,13 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
     const float* r0 = T + (OFF_machu_v + __umul24((unsigned)(sm.i - 1), 2u * MACHU_NT));
 #pragma unroll
     for (int k = 0; k + 1 < MACHU_NT; k += 2) {
-      const f2v r = blend2(sm.f, ld2(r0 + k), ld2(r0 + MACHU_NT + k));
+      const f2v r = blend2(sm.f, ld2(r0 + 2 * k), ld2(r0 + 2 * k + 2));
       MU[k] = r.x; MU[k + 1] = r.y;
     }
-    if (MACHU_NT & 1) MU[MACHU_NT - 1] = blend(sm.f, r0[MACHU_NT - 1], r0[2 * MACHU_NT - 1]);
+    if (MACHU_NT & 1) {
+      const f2v t = ld2(r0 + 2 * MACHU_NT - 2);
+      MU[MACHU_NT - 1] = blend(sm.f, t.x, t.y);
+    }
   }
   const float CDmach = MU[MU_CDmach], CYb_M = MU[MU_CYb_M], Clb_M = MU[MU_Clb_M];
   const float Clda_M = MU[MU_Clda_M], Cldr_M = MU[MU_Cldr_M], Cma_M = MU[MU_Cma_M];
@@ -1241,18 +1263,22 @@ __device__ __forceinline__ void aero(const AeroIn& a, const float* T, float* F6)
 template <bool LOWREG = false, bool WIND = true>
 __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, double& se, const AltRef& A,
                                       const float* T, const ModelConsts& C, bool ic F16_STAMP_ARG) {
-  const float dt = (float)C.dt;
+  const float dt = C.dt_f;
   const FcsTab tb = fcs_tables(L, T);
   if (!ic) {
     // -- FGPropagate: integrate with the previous frame's derivatives --
-    const float hx = 0.5f * dt * L.wI[0], hy = 0.5f * dt * L.wI[1], hz = 0.5f * dt * L.wI[2];
-    const float a2 = hx * hx + hy * hy + hz * hz;
+    const float hx = C.half_dt * L.wI[0], hy = C.half_dt * L.wI[1], hz = C.half_dt * L.wI[2];
+    const float a2 = hx * hx + hy * hy + hz * hz;  // = fma(hz, hz, fma(hx, hx, hy hy)) (contraction)
     // QExp: cos(a), sin(a)/a; series through a^8 (error < 3e-10 for |a| < 0.5, i.e. body
     // rates below 120 rad/s), exact functions beyond
     // (the same nested FMAs, each level fma(-a2, t, k), written with -a2 as a value so that every
     // level after the first is one v_fmaak_f32 (a VOP2 form takes the literal; the VOP3 FMA with
     // a negated operand needs the constant moved into a register first))
-    const float na2 = -a2;
+    // (-a2 formed as its own sum of negated products, exactly -a2, and made opaque by an empty
+    // asm: left as "-a2" the compiler folds the negation back into VOP3 operand modifiers, and
+    // the polynomial's constants then need registers instead of the v_fmaak literal)
+    float na2 = __builtin_fmaf(-hz, hz, __builtin_fmaf(-hx, hx, -(hy * hy)));
+    if constexpr (!LOWREG) asm("" : "+v"(na2));
     float ca, sa;
     if constexpr (LOWREG) {  // (pre-round-5 form: the same values)
       ca = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f - a2 * (1.0f / 40320.0f))));
@@ -1265,10 +1291,11 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
                                                                                    1.0f / 5040.0f),
                                                                  1.0f / 120.0f), 1.0f / 6.0f), 1.0f);
     }
-    if (__builtin_expect(a2 >= 0.25f, 0)) {
-      const float ang = fsqrt(a2);
-      ca = cosf(ang);
-      sa = sinf(ang) / ang;
+    if (__builtin_expect(na2 <= -0.25f, 0)) {  // a2 >= 1/4
+      const float ang = fsqrt(-na2);
+      float sn;
+      sincosf(ang, &sn, &ca);  // (one OCML argument reduction for both)
+      sa = sn / ang;
     }
     const float p0 = ca, p1 = hx * sa, p2 = hy * sa, p3 = hz * sa;
     // n = q (x) p, as the scalar statement
@@ -1309,7 +1336,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     // AB2 velocity: v += dt (1.5 a - 0.5 ap)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const float corr = (dt * (1.0f / 12.0f)) * (-16.0f * L.dv1[j] + 5.0f * L.dv2[j]);
+      const float corr = C.dt_12 * (-16.0f * L.dv1[j] + 5.0f * L.dv2[j]);
       L.rI[j] += C.dt * L.vI[j] + (double)corr;
       const float dv = dt * (1.5f * L.aI[j] - 0.5f * L.aIp[j]);
       L.vI[j] += (double)dv;
@@ -1317,7 +1344,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
       L.dv1[j] = -dv;
       L.aIp[j] = L.aI[j];
     }
-    L.epa += OMEGA_E * C.dt;
+    L.epa += C.epa_dt;
     const double c2 = ce * C.cos_dE - se * C.sin_dE;
     const double s2 = se * C.cos_dE + ce * C.sin_dE;
     ce = c2; se = s2;
@@ -1337,7 +1364,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   // straight-line code instead of two divergent branches around the polynomials
   const float alpha = fatan2<LOWREG>(moving ? wa : 0.0f, ua);
   const float suw = fsqrt(muw);
-  const float beta = fatan2<LOWREG>(moving ? va : 0.0f, suw);
+  const float beta = fatan2<LOWREG, true>(moving ? va : 0.0f, suw);  // (suw = sqrt of a sum of squares)
   const float iuw = rcpf(suw), ivt = rcpf(vt);
   const float ca_ = moving ? ua * iuw : 1.0f, sa_ = moving ? wa * iuw : 0.0f;
   const float cb_ = moving ? suw * ivt : 1.0f, sb_ = moving ? va * ivt : 0.0f;

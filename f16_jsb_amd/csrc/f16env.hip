@@ -798,7 +798,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       L.step = __float_as_int(e.x); L.ep_count = __float_as_int(e.y); L.ep_ret = f2d(e.z, e.w);
       const float4 w = stash[128 + lane];
       L.epa = f2d(w.x, w.y);
-      for (int s = 0; s < a.E.down_sample; ++s) L.epa += OMEGA_E * a.C.dt;  // frame()'s per-frame advance
+      for (int s = 0; s < a.E.down_sample; ++s) L.epa += a.C.epa_dt;  // frame()'s per-frame advance
       if (GUST) {
         const float4 u = stash[192 + lane];
         L.gust[0] = w.z; L.gust[1] = w.w; L.gust[2] = u.x; L.wst[0] = u.y; L.wst[1] = u.z; L.wst[2] = u.w;
@@ -2221,6 +2221,20 @@ static void build_consts(const f16env_config& cfg, ModelConsts& C) {
   C.dt = cfg.dt;
   C.cos_dE = cos(OMEGA_E * cfg.dt);
   C.sin_dE = sin(OMEGA_E * cfg.dt);
+  C.epa_dt = OMEGA_E * cfg.dt;
+  // fp32 products the frames formerly formed per frame (f16_device.h kin2 / pidf / frame): the
+  // same single fp32 roundings, here in host IEEE arithmetic
+  const float dt = (float)cfg.dt;
+  C.dt_f = dt;
+  C.half_dt = 0.5f * dt;
+  C.dt_12 = dt * (1.0f / 12.0f);
+  C.lim_ail = dt * (2.0f / 0.3f);
+  C.lim_rud = dt * (2.0f / 0.4f);
+  C.lim_lef = dt * (2.0f / 3.0f);
+  C.lim_sb = dt * 60.0f;
+  C.kidt_roll = 0.0005f * dt;
+  C.kidt_pitch = 0.025f * dt;
+  C.kidt_yaw = 0.00001f * dt;
 }
 
 static EnvArgs env_args(const f16env* h) {

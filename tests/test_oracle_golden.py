@@ -103,6 +103,17 @@ def _slopes(v):
     return v, d
 
 
+def _pair_slot(j, g):
+    """(value, slope) float offsets of table j within a g-table entry: g values then g slopes for
+    even g (tools/gen_tables.py put_rows), pairwise -- (2 values | 2 slopes) per table pair, an odd
+    last table as (value | slope) -- for odd g"""
+    if g % 2 == 0:
+        return j, g + j
+    c = j - j % 2
+    w = min(2, g - c)
+    return 2 * c + j % 2, 2 * c + w + j % 2
+
+
 def test_kernel_blob_matches_fixture():
     """The fp32 LDS blob in f16_tables.h holds exactly the fixture's tables (rounded to fp32),
     each beside its fp32 slope along the first interpolation axis (value, slope layout)."""
@@ -121,11 +132,12 @@ def test_kernel_blob_matches_fixture():
     for key, names, ncol in (("ade", ["CDDh", "CLDh", "CmDh"], 5), ("ab13", ["Clb", "Cnb"], 13),
                              ("ab7", ["Clda", "Cldr", "Cnda", "Cndr"], 7)):
         g = len(names)
-        for j, n in enumerate(names):  # [12][ncol][g values | g alpha-slopes]
+        for j, n in enumerate(names):  # [12][ncol][g values | g alpha-slopes]; odd g pairwise
             v, d = _slopes(fns[n]["table"]["data"])
             base = offs[key] + (np.arange(12)[:, None] * ncol + np.arange(ncol)[None, :]) * 2 * g
-            np.testing.assert_array_equal(blob[base + j], v)
-            np.testing.assert_array_equal(blob[base + g + j], d)
+            vo, so = _pair_slot(j, g)
+            np.testing.assert_array_equal(blob[base + vo], v)
+            np.testing.assert_array_equal(blob[base + so], d)
     # engine: (mach x density-alt) union grid [14][8][3 values | 3 mach-slopes], Idle/Mil rows
     # clamped at their last mach row
     eng = m["engine"]["tables"]
@@ -135,8 +147,18 @@ def test_kernel_blob_matches_fixture():
         full = t[np.minimum(np.arange(len(rows)), len(t) - 1)]
         v, d = _slopes(full)
         base = offs["engu_v"] + (np.arange(len(rows))[:, None] * 8 + np.arange(8)[None, :]) * 6
-        np.testing.assert_array_equal(blob[base + j], v)
-        np.testing.assert_array_equal(blob[base + 3 + j], d)
+        vo, so = _pair_slot(j, 3)
+        np.testing.assert_array_equal(blob[base + vo], v)
+        np.testing.assert_array_equal(blob[base + so], d)
+    # the nine Mach tables on their union grid, [13][pairwise 9 values / mach-slopes]: checked as
+    # a pure re-layout of the blob order the kernel's blends read (value, slope per table)
+    nt, nu = 9, 13
+    for j in range(nt):
+        vo, so = _pair_slot(j, nt)
+        v = blob[offs["machu_v"] + np.arange(nu) * 2 * nt + vo]
+        d = blob[offs["machu_v"] + np.arange(nu) * 2 * nt + so]
+        np.testing.assert_array_equal(d[:-1], (v[1:] - v[:-1]).astype(np.float32))
+        assert d[-1] == 0.0
     v, d = _slopes(m["kCLge"]["data"])
     np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v))], v)
     np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v)) + 1], d)

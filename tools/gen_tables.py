@@ -307,23 +307,30 @@ def emit_kernel(model, path):
     # Every table is stored as (value, slope) along the interpolation axis the kernel blends
     # first: slope[i] = f32(v[i+1]) - f32(v[i]) (fp32 arithmetic, 0 on the last row), so a
     # lerp is one FMA v + f * slope -- bit-identical to f * (v1 - v0) + v0 computed in-kernel.
-    def put_rows(key, rows_vals, group):
+    def put_rows(key, rows_vals, group, pairwise=False):
         """rows over the interpolation axis, each a list of entries of `group` values; emitted
-        per (row, entry) as the group's values then its slopes"""
+        per (row, entry) as the group's values then its slopes -- or, pairwise (odd groups),
+        per pair of tables as their two values then their two slopes (an odd last table as its
+        value, slope), so that every (value, value) and (slope, slope) pair a packed blend reads
+        sits at an even float offset: an aligned register pair straight from the LDS read"""
         v = [np.array(r, np.float64).astype(np.float32) for r in rows_vals]
         vals = []
         for i in range(len(v)):
             d = (v[i + 1] - v[i]) if i + 1 < len(v) else np.zeros_like(v[i])
             for e in range(len(v[i]) // group):
-                vals += [float(x) for x in v[i][e * group:(e + 1) * group]]
-                vals += [float(x) for x in d[e * group:(e + 1) * group]]
+                step = 2 if pairwise else group
+                for c in range(e * group, (e + 1) * group, step):
+                    hi = min(c + step, (e + 1) * group)
+                    vals += [float(x) for x in v[i][c:hi]]
+                    vals += [float(x) for x in d[c:hi]]
         put(key, vals)
 
     # alpha-1D tables: [12 alpha][16 values | 16 slopes]
     put_rows("alpha1d", [[fns[n]["table"]["data"][i] for n in ALPHA_1D] for i in range(12)], len(ALPHA_1D))
-    # 2-D over (alpha, X): [12 alpha][X][group values | group alpha-slopes]
+    # 2-D over (alpha, X): [12 alpha][X][group values | group alpha-slopes]; the 3-table group
+    # (alpha, elevator) pairwise: [2 values | 2 alpha-slopes | value | alpha-slope]
     put_rows("ade", [[fns[n]["table"]["data"][i][j] for j in range(len(de_bp)) for n in ALPHA_DE_2D]
-                     for i in range(12)], len(ALPHA_DE_2D))
+                     for i in range(12)], len(ALPHA_DE_2D), pairwise=True)
     put_rows("ab13", [[fns[n]["table"]["data"][i][j] for j in range(len(b13)) for n in ALPHA_BETA13]
                       for i in range(12)], len(ALPHA_BETA13))
     put_rows("ab7", [[fns[n]["table"]["data"][i][j] for j in range(len(b7)) for n in ALPHA_BETA7]
@@ -343,9 +350,9 @@ def emit_kernel(model, path):
         return data[i - 1] + f * (data[i] - data[i - 1])
 
     mach_u = sorted({b for n in MACH_1D for b in fns[n]["table"]["rows"]})
-    # [13 mach][9 values | 9 slopes]
+    # [13 mach][(2 values | 2 slopes) x 4, value | slope]
     put_rows("machu_v", [[interp_clamped(fns[n]["table"]["rows"], fns[n]["table"]["data"], x) for n in MACH_1D]
-                         for x in mach_u], len(MACH_1D))
+                         for x in mach_u], len(MACH_1D), pairwise=True)
     eng_rows = model["engine"]["tables"]["AugThrust"]["rows"]
     eng_cols = model["engine"]["tables"]["AugThrust"]["cols"]
     eng_names = ("IdleThrust", "MilThrust", "AugThrust")
@@ -362,8 +369,8 @@ def emit_kernel(model, path):
                 ii = min(i, len(t["rows"]) - 1)  # FGTable clamps the row factor at the last row
                 row.append(t["data"][ii][j])
         eng_u.append(row)
-    # [14 mach][8 density-alt][3 values | 3 mach-slopes]
-    put_rows("engu_v", eng_u, len(eng_names))
+    # [14 mach][8 density-alt][2 values | 2 mach-slopes | value | mach-slope]
+    put_rows("engu_v", eng_u, len(eng_names), pairwise=True)
     # small 1-D tables: (value, slope) pairs
     put_rows("kclge_vd", [[v] for v in model["kCLge"]["data"]], 1)
     for n, t in model["fcs_tables"].items():

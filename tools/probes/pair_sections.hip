@@ -59,9 +59,9 @@ __global__ void k_blends(const float* __restrict__ in, float* __restrict__ out, 
   {
     const float* p0 = sT + OFF_ade + ((sa.i - 1) * F16_N_DE + se.i - 1) * 6;
     const float* p1 = p0 + 6;
-    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 3)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 3));
+    const f2v c1 = blend2(sa.f, ld2(p0), ld2(p0 + 2)), c2 = blend2(sa.f, ld2(p1), ld2(p1 + 2));
     const f2v r = blend2(se.f, c1, c2 - c1);
-    const float d1 = blend(sa.f, p0[2], p0[5]), d2 = blend(sa.f, p1[2], p1[5]);
+    const float d1 = blend(sa.f, p0[4], p0[5]), d2 = blend(sa.f, p1[4], p1[5]);
     acc += r.x + r.y + (d1 + se.f * (d2 - d1));
   }
   const Seg sb13 = bracket(BP_beta13_bp, sT + OFF_pair_beta13, a.beta);
@@ -91,10 +91,10 @@ __global__ void k_blends(const float* __restrict__ in, float* __restrict__ out, 
     const float* r0 = sT + OFF_machu_v + (sm.i - 1) * (2 * MACHU_NT);
 #pragma unroll
     for (int q = 0; q + 1 < MACHU_NT; q += 2) {
-      const f2v r = blend2(sm.f, ld2(r0 + q), ld2(r0 + MACHU_NT + q));
+      const f2v r = blend2(sm.f, ld2(r0 + 2 * q), ld2(r0 + 2 * q + 2));
       acc += r.x + r.y;
     }
-    if (MACHU_NT & 1) acc += blend(sm.f, r0[MACHU_NT - 1], r0[2 * MACHU_NT - 1]);
+    if (MACHU_NT & 1) acc += blend(sm.f, r0[2 * MACHU_NT - 2], r0[2 * MACHU_NT - 1]);
   }
   out[k] = acc;
 }
