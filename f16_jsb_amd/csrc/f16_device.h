@@ -182,7 +182,7 @@ static constexpr float RAD2DEG_F = 57.295779513082320876798f;
 //   C1  rI.z vI.x (f64)        C7  q0 q1 q2 q3            C13 alpha beta mach qc      (latch)
 //   C2  vI.y vI.z (f64)        C8  wI.xyz wId.x           C14 npy npz goal.x goal.y   (latch, goal)
 //   C3  epa ep_ret (f64)       C9  wId.yz ba.y ba.z       C15 goal.z last_d' step ep_count (i32)
-//   C4  dv1.xyz dv2.x          C10 tef ail ele rud        C16 steady wind.xyz, 0  (wind kernels only)
+//   C4  ndv1.xyz dv2.x         C10 tef ail ele rud        C16 steady wind.xyz, 0  (wind kernels only)
 //   C5  dv2.yz aI.xy           C11 lef sb pid_r_i pid_r_p C17 gust.xyz, 0         (wind kernels only)
 // n2' = N2 with the augmentation flag in its sign bit (N2 >= 60 %), last_d' = last distance
 // with the FRESH flag in its sign bit (a norm, >= 0). Not stored, because a step never reads
@@ -210,7 +210,9 @@ struct SoA {
 
 struct Lane {
   double rI[3], vI[3], epa, ep_ret;
-  float dv1[3], dv2[3], aI[3], aIp[3], q[4], wI[3], wId[3], ba[3];
+  // ndv1 = -dv1: the AB3 history kept negated (= the last frame's velocity increment), which the
+  // frame then stores without a negation per component
+  float ndv1[3], dv2[3], aI[3], aIp[3], q[4], wI[3], wId[3], ba[3];
   float tef, ail, ele, rud, lef, sb;
   float pri, prp, ppi, ppp, pyi, pyp;
   float n1, n2;
@@ -296,7 +298,7 @@ __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, f
   L.rI[2] = f2d(c[1].x, c[1].y); L.vI[0] = f2d(c[1].z, c[1].w);
   L.vI[1] = f2d(c[2].x, c[2].y); L.vI[2] = f2d(c[2].z, c[2].w);
   L.epa = f2d(c[3].x, c[3].y); L.ep_ret = f2d(c[3].z, c[3].w);
-  L.dv1[0] = c[4].x; L.dv1[1] = c[4].y; L.dv1[2] = c[4].z; L.dv2[0] = c[4].w;
+  L.ndv1[0] = c[4].x; L.ndv1[1] = c[4].y; L.ndv1[2] = c[4].z; L.dv2[0] = c[4].w;
   L.dv2[1] = c[5].x; L.dv2[2] = c[5].y; L.aI[0] = c[5].z; L.aI[1] = c[5].w;
   L.aI[2] = c[6].x; L.aIp[0] = c[6].y; L.aIp[1] = c[6].z; L.aIp[2] = c[6].w;
   L.q[0] = c[7].x; L.q[1] = c[7].y; L.q[2] = c[7].z; L.q[3] = c[7].w;
@@ -355,7 +357,7 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   c[1] = make_float4(dlo(L.rI[2]), dhi(L.rI[2]), dlo(L.vI[0]), dhi(L.vI[0]));
   c[2] = make_float4(dlo(L.vI[1]), dhi(L.vI[1]), dlo(L.vI[2]), dhi(L.vI[2]));
   c[3] = make_float4(dlo(L.epa), dhi(L.epa), dlo(L.ep_ret), dhi(L.ep_ret));
-  c[4] = make_float4(L.dv1[0], L.dv1[1], L.dv1[2], L.dv2[0]);
+  c[4] = make_float4(L.ndv1[0], L.ndv1[1], L.ndv1[2], L.dv2[0]);
   c[5] = make_float4(L.dv2[1], L.dv2[2], L.aI[0], L.aI[1]);
   c[6] = make_float4(L.aI[2], L.aIp[0], L.aIp[1], L.aIp[2]);
   c[7] = make_float4(L.q[0], L.q[1], L.q[2], L.q[3]);
@@ -556,6 +558,13 @@ __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
 // mixed-sign or swapped operand pairs into v_mov / v_xor shuffles; these spell the half selects
 // (op_sel: the half of each source feeding the low result, op_sel_hi: the high result) and the
 // per-half negations out. MODS is the modifier string, e.g. "op_sel:[1,1] op_sel_hi:[1,0]".
+// packed-chain switches (A/B builds: -DF16_PK_DERIVE=0 / -DF16_PK_FORCE=0 restore the scalar forms)
+#ifndef F16_PK_DERIVE
+#define F16_PK_DERIVE 0
+#endif
+#ifndef F16_PK_FORCE
+#define F16_PK_FORCE 0
+#endif
 #define PK_FMA(d, a, b, c, MODS) asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(d) : "v"(a), "v"(b), "v"(c))
 #define PK_MUL(d, a, b, MODS) asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(d) : "v"(a), "v"(b))
 
@@ -854,6 +863,11 @@ __device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRe
 // advanced within the step along the geodetic normal: h = h0 + n . (rE - r0). Over one env
 // step |rE - r0| < 70 ft, so the neglected curvature term |dr|^2/2R < 2e-4 ft (far below the
 // 4e-4 ft fp32 resolution of the observed altitude).
+// PK (the one-wave builds): Ti2b's rows 0 and 1 as register pairs (T0, T3), (T1, T4), (T2, T5),
+// and uvw[0..1] as packed FMAs, per half the scalar product and FMAs in the same order (the same
+// roundings). (Tl2b's third column likewise cost more than it saved: the frames read only its
+// elements 2 and 8, the aero reference point having no lateral offset.)
+template <bool PK = false>
 __device__ __forceinline__ void derive(const Lane& L, double ce, double se, const AltRef& A, Derived& d) {
   const double xE = ce * L.rI[0] + se * L.rI[1];
   const double yE = -se * L.rI[0] + ce * L.rI[1];
@@ -899,7 +913,34 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
   mvec(d.Ti2b, vr, d.uvw);
   // vPQR = vPQRi - Ti2b * (0,0,w)
   pqr_aero(L.q, L.wI, d.pqr);
-  d.vg = ground_speed(vr[0], vr[1], vr[2], (float)L.rI[0], (float)L.rI[1], (float)L.rI[2]);
+  d.vg = ground_speed(vr[0], vr[1], vr[2], xi, yi, zf);
+  if constexpr (PK && F16_PK_DERIVE) {
+    // velocity and position components paired per axis, (v_j, r_j): the broadcast velocity
+    // operand of the row products and both factors of ground_speed's v.r and r.r
+    const f2v R0 = {d.Ti2b[0], d.Ti2b[3]}, R1 = {d.Ti2b[1], d.Ti2b[4]}, R2 = {d.Ti2b[2], d.Ti2b[5]};
+    const f2v P0 = {vr[0], xi}, P1 = {vr[1], yi}, P2 = {vr[2], zf};
+    f2v m, u;
+#if F16_PK_DERIVE == 2  // (A/B: vector builtins, the broadcasts left to the compiler's op_sel folding)
+    m = R0 * f2v{P0.x, P0.x};
+    m = __builtin_elementwise_fma(R1, f2v{P1.x, P1.x}, m);
+    u = __builtin_elementwise_fma(R2, f2v{P2.x, P2.x}, m);
+    d.uvw[0] = u.x; d.uvw[1] = u.y;
+    m = P1 * f2v{P1.y, P1.y};
+    m = __builtin_elementwise_fma(P0, f2v{P0.y, P0.y}, m);
+    m = __builtin_elementwise_fma(P2, f2v{P2.y, P2.y}, m);
+#else
+    PK_MUL(m, R0, P0, "op_sel:[0,0] op_sel_hi:[1,0]");             // T[3i] v0
+    PK_FMA(m, R1, P1, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+1] v1
+    PK_FMA(u, R2, P2, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+2] v2
+    d.uvw[0] = u.x; d.uvw[1] = u.y;
+    // ground_speed's (v.r, r.r) = fma(., z, fma(., x, . y)) per half
+    PK_MUL(m, P1, P1, "op_sel:[0,1] op_sel_hi:[1,1]");             // (vy ry, ry ry)
+    PK_FMA(m, P0, P0, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vx rx, rx rx)
+    PK_FMA(m, P2, P2, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vz rz, rz rz)
+#endif
+    const float vv = vr[0] * vr[0] + vr[1] * vr[1] + vr[2] * vr[2];
+    d.vg = __builtin_amdgcn_sqrtf(fmaxf(vv - m.x * m.x * __builtin_amdgcn_rcpf(m.y), 0.0f));
+  }
   // J2 gravity (FGInertial::GetGravityJ2), ECEF
   const float adivr = (float)WGS_A * inv_r;
   const float pre = 1.5f * (float)J2_E * adivr * adivr;
@@ -1336,12 +1377,13 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     // AB2 velocity: v += dt (1.5 a - 0.5 ap)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const float corr = C.dt_12 * (-16.0f * L.dv1[j] + 5.0f * L.dv2[j]);
+      // (16 ndv1 = -16 dv1 exactly: the same FMA, the same rounding)
+      const float corr = C.dt_12 * (16.0f * L.ndv1[j] + 5.0f * L.dv2[j]);
       L.rI[j] += C.dt * L.vI[j] + (double)corr;
       const float dv = dt * (1.5f * L.aI[j] - 0.5f * L.aIp[j]);
       L.vI[j] += (double)dv;
-      L.dv2[j] = L.dv1[j] - dv;
-      L.dv1[j] = -dv;
+      L.dv2[j] = -L.ndv1[j] - dv;  // dv1 - dv
+      L.ndv1[j] = dv;              // dv1 = -dv
       L.aIp[j] = L.aI[j];
     }
     L.epa += C.epa_dt;
@@ -1351,7 +1393,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   }
   F16_STAMP(stamps, ST_PROP);
   Derived d;
-  derive(L, ce, se, A, d);
+  derive<!LOWREG>(L, ce, se, A, d);
   F16_STAMP(stamps, ST_DERIVE);
   // -- Auxiliary, wind-axis part (needs no atmosphere) --
   float wb[3] = {0.0f, 0.0f, 0.0f};
@@ -1410,9 +1452,23 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   // wind (D, Y, L) -> body, vFw = (-D, Y, -L)
   const float fw0 = -A6[0], fw1 = A6[1], fw2 = -A6[2];
   float F[3], M[3];
-  F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
+  if constexpr (LOWREG || !F16_PK_FORCE) {
+    F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
+    F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
+  } else {
+    // F[0] and F[2] in one packed chain, per half the scalar statement's contraction
+    //   F0 = fma(-sa, fw2, fma(ca cb, fw0, -(ca sb fw1)))   F2 = fma(ca, fw2, fma(sa cb, fw0, -(sa sb fw1)))
+    // with fw0 = -D, fw1 = Y, fw2 = -L (the negations as operand modifiers: exact)
+    const f2v CS = {ca_, sa_}, B = {cb_, sb_}, W = {A6[0], A6[1]}, LL = {A6[2], A6[3]};
+    f2v pcb, psb, r;
+    PK_MUL(pcb, CS, B, "op_sel:[0,0] op_sel_hi:[1,0]");                                 // (ca cb, sa cb)
+    PK_MUL(psb, CS, B, "op_sel:[0,1] op_sel_hi:[1,1]");                                 // (ca sb, sa sb)
+    PK_MUL(psb, psb, W, "op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[1,0] neg_hi:[1,0]");      // -(. Y)
+    PK_FMA(r, pcb, W, psb, "op_sel:[0,0,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]");  // + . (-D)
+    PK_FMA(r, CS, LL, r, "op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]");           // + (sa L, -ca L)
+    F[0] = r.x; F[2] = r.y;
+  }
   F[1] = sb_ * fw0 + cb_ * fw1;
-  F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
   float rxF[3];
   cross_c(MP.rp, F, rxF);
   M[0] = A6[3] + rxF[0];

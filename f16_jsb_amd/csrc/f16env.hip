@@ -254,7 +254,7 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   L.wI[1] = (float)(ic[F16_IC_Q_RPS] + T5 * OMEGA_E);
   L.wI[2] = (float)(ic[F16_IC_R_RPS] + T8 * OMEGA_E);
   for (int j = 0; j < 3; ++j) {
-    L.wId[j] = 0.0f; L.ba[j] = 0.0f; L.aI[j] = 0.0f; L.aIp[j] = 0.0f; L.dv1[j] = 0.0f; L.dv2[j] = 0.0f;
+    L.wId[j] = 0.0f; L.ba[j] = 0.0f; L.aI[j] = 0.0f; L.aIp[j] = 0.0f; L.ndv1[j] = -0.0f; L.dv2[j] = 0.0f;
     L.wst[j] = (float)ic[F16_IC_WIND_N_FPS + j];
     L.wind[j] = L.wst[j] + L.gust[j];  // callers set the gust (0 outside the cfg5 gust mode)
   }
@@ -274,7 +274,7 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   // once and hit twice
 #pragma nounroll
   for (int pass = 0; pass < 3; ++pass) frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
-  for (int j = 0; j < 3; ++j) { L.dv1[j] = 0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }
+  for (int j = 0; j < 3; ++j) { L.ndv1[j] = -0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }  // (dv1 = +0)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1657,7 +1657,7 @@ __global__ void f16_get_state_kernel(SoA s, double* c, ModelConsts C) {
   double* o = c + (int64_t)F16C_N * k;
   for (int j = 0; j < 3; ++j) {
     o[F16C_RI + j] = L.rI[j]; o[F16C_VI + j] = L.vI[j];
-    o[F16C_VIH1 + j] = L.vI[j] + (double)L.dv1[j];
+    o[F16C_VIH1 + j] = L.vI[j] - (double)L.ndv1[j];  // vI + dv1
     o[F16C_VIH2 + j] = L.vI[j] + (double)L.dv2[j];
     o[F16C_AI + j] = L.aI[j]; o[F16C_AIP + j] = L.aIp[j]; o[F16C_WI + j] = L.wI[j];
     o[F16C_WID + j] = L.wId[j]; o[F16C_BA + j] = L.ba[j]; o[F16C_GOAL + j] = L.goal[j];
@@ -1684,7 +1684,7 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int*
   const double* o = c + (int64_t)F16C_N * k;
   for (int j = 0; j < 3; ++j) {
     L.rI[j] = o[F16C_RI + j]; L.vI[j] = o[F16C_VI + j];
-    L.dv1[j] = (float)(o[F16C_VIH1 + j] - o[F16C_VI + j]);
+    L.ndv1[j] = -(float)(o[F16C_VIH1 + j] - o[F16C_VI + j]);
     L.dv2[j] = (float)(o[F16C_VIH2 + j] - o[F16C_VI + j]);
     L.aI[j] = (float)o[F16C_AI + j]; L.aIp[j] = (float)o[F16C_AIP + j]; L.wI[j] = (float)o[F16C_WI + j];
     L.wId[j] = (float)o[F16C_WID + j]; L.ba[j] = (float)o[F16C_BA + j]; L.goal[j] = (float)o[F16C_GOAL + j];
