@@ -558,12 +558,9 @@ __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
 // mixed-sign or swapped operand pairs into v_mov / v_xor shuffles; these spell the half selects
 // (op_sel: the half of each source feeding the low result, op_sel_hi: the high result) and the
 // per-half negations out. MODS is the modifier string, e.g. "op_sel:[1,1] op_sel_hi:[1,0]".
-// packed-chain switches (A/B builds: -DF16_PK_DERIVE=0 / -DF16_PK_FORCE=0 restore the scalar forms)
+// packed-chain switch (A/B builds: -DF16_PK_DERIVE=0 restores the scalar forms)
 #ifndef F16_PK_DERIVE
-#define F16_PK_DERIVE 0
-#endif
-#ifndef F16_PK_FORCE
-#define F16_PK_FORCE 0
+#define F16_PK_DERIVE 1
 #endif
 #define PK_FMA(d, a, b, c, MODS) asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(d) : "v"(a), "v"(b), "v"(c))
 #define PK_MUL(d, a, b, MODS) asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(d) : "v"(a), "v"(b))
@@ -920,15 +917,6 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
     const f2v R0 = {d.Ti2b[0], d.Ti2b[3]}, R1 = {d.Ti2b[1], d.Ti2b[4]}, R2 = {d.Ti2b[2], d.Ti2b[5]};
     const f2v P0 = {vr[0], xi}, P1 = {vr[1], yi}, P2 = {vr[2], zf};
     f2v m, u;
-#if F16_PK_DERIVE == 2  // (A/B: vector builtins, the broadcasts left to the compiler's op_sel folding)
-    m = R0 * f2v{P0.x, P0.x};
-    m = __builtin_elementwise_fma(R1, f2v{P1.x, P1.x}, m);
-    u = __builtin_elementwise_fma(R2, f2v{P2.x, P2.x}, m);
-    d.uvw[0] = u.x; d.uvw[1] = u.y;
-    m = P1 * f2v{P1.y, P1.y};
-    m = __builtin_elementwise_fma(P0, f2v{P0.y, P0.y}, m);
-    m = __builtin_elementwise_fma(P2, f2v{P2.y, P2.y}, m);
-#else
     PK_MUL(m, R0, P0, "op_sel:[0,0] op_sel_hi:[1,0]");             // T[3i] v0
     PK_FMA(m, R1, P1, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+1] v1
     PK_FMA(u, R2, P2, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+2] v2
@@ -937,7 +925,6 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
     PK_MUL(m, P1, P1, "op_sel:[0,1] op_sel_hi:[1,1]");             // (vy ry, ry ry)
     PK_FMA(m, P0, P0, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vx rx, rx rx)
     PK_FMA(m, P2, P2, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vz rz, rz rz)
-#endif
     const float vv = vr[0] * vr[0] + vr[1] * vr[1] + vr[2] * vr[2];
     d.vg = __builtin_amdgcn_sqrtf(fmaxf(vv - m.x * m.x * __builtin_amdgcn_rcpf(m.y), 0.0f));
   }
@@ -1452,22 +1439,10 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   // wind (D, Y, L) -> body, vFw = (-D, Y, -L)
   const float fw0 = -A6[0], fw1 = A6[1], fw2 = -A6[2];
   float F[3], M[3];
-  if constexpr (LOWREG || !F16_PK_FORCE) {
-    F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
-    F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
-  } else {
-    // F[0] and F[2] in one packed chain, per half the scalar statement's contraction
-    //   F0 = fma(-sa, fw2, fma(ca cb, fw0, -(ca sb fw1)))   F2 = fma(ca, fw2, fma(sa cb, fw0, -(sa sb fw1)))
-    // with fw0 = -D, fw1 = Y, fw2 = -L (the negations as operand modifiers: exact)
-    const f2v CS = {ca_, sa_}, B = {cb_, sb_}, W = {A6[0], A6[1]}, LL = {A6[2], A6[3]};
-    f2v pcb, psb, r;
-    PK_MUL(pcb, CS, B, "op_sel:[0,0] op_sel_hi:[1,0]");                                 // (ca cb, sa cb)
-    PK_MUL(psb, CS, B, "op_sel:[0,1] op_sel_hi:[1,1]");                                 // (ca sb, sa sb)
-    PK_MUL(psb, psb, W, "op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[1,0] neg_hi:[1,0]");      // -(. Y)
-    PK_FMA(r, pcb, W, psb, "op_sel:[0,0,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]");  // + . (-D)
-    PK_FMA(r, CS, LL, r, "op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]");           // + (sa L, -ca L)
-    F[0] = r.x; F[2] = r.y;
-  }
+  F[0] = ca_ * cb_ * fw0 - ca_ * sb_ * fw1 - sa_ * fw2;
+  F[2] = sa_ * cb_ * fw0 - sa_ * sb_ * fw1 + ca_ * fw2;
+  // (F[0] and F[2] as one packed chain -- five VOP3P instructions for ten, bit-identical -- cost
+  // +0.7 us per step on a same-box A/B, profiles/r05_ab_pk_variants.json "noder": not used)
   F[1] = sb_ * fw0 + cb_ * fw1;
   float rxF[3];
   cross_c(MP.rp, F, rxF);
