@@ -558,10 +558,6 @@ __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
 // mixed-sign or swapped operand pairs into v_mov / v_xor shuffles; these spell the half selects
 // (op_sel: the half of each source feeding the low result, op_sel_hi: the high result) and the
 // per-half negations out. MODS is the modifier string, e.g. "op_sel:[1,1] op_sel_hi:[1,0]".
-// packed-chain switch (A/B builds: -DF16_PK_DERIVE=0 restores the scalar forms)
-#ifndef F16_PK_DERIVE
-#define F16_PK_DERIVE 1
-#endif
 #define PK_FMA(d, a, b, c, MODS) asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(d) : "v"(a), "v"(b), "v"(c))
 #define PK_MUL(d, a, b, MODS) asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(d) : "v"(a), "v"(b))
 
@@ -860,11 +856,6 @@ __device__ __forceinline__ void alt_ref_init(double x, double y, double z, AltRe
 // advanced within the step along the geodetic normal: h = h0 + n . (rE - r0). Over one env
 // step |rE - r0| < 70 ft, so the neglected curvature term |dr|^2/2R < 2e-4 ft (far below the
 // 4e-4 ft fp32 resolution of the observed altitude).
-// PK (the one-wave builds): Ti2b's rows 0 and 1 as register pairs (T0, T3), (T1, T4), (T2, T5),
-// and uvw[0..1] as packed FMAs, per half the scalar product and FMAs in the same order (the same
-// roundings). (Tl2b's third column likewise cost more than it saved: the frames read only its
-// elements 2 and 8, the aero reference point having no lateral offset.)
-template <bool PK = false>
 __device__ __forceinline__ void derive(const Lane& L, double ce, double se, const AltRef& A, Derived& d) {
   const double xE = ce * L.rI[0] + se * L.rI[1];
   const double yE = -se * L.rI[0] + ce * L.rI[1];
@@ -911,23 +902,6 @@ __device__ __forceinline__ void derive(const Lane& L, double ce, double se, cons
   // vPQR = vPQRi - Ti2b * (0,0,w)
   pqr_aero(L.q, L.wI, d.pqr);
   d.vg = ground_speed(vr[0], vr[1], vr[2], xi, yi, zf);
-  if constexpr (PK && F16_PK_DERIVE) {
-    // velocity and position components paired per axis, (v_j, r_j): the broadcast velocity
-    // operand of the row products and both factors of ground_speed's v.r and r.r
-    const f2v R0 = {d.Ti2b[0], d.Ti2b[3]}, R1 = {d.Ti2b[1], d.Ti2b[4]}, R2 = {d.Ti2b[2], d.Ti2b[5]};
-    const f2v P0 = {vr[0], xi}, P1 = {vr[1], yi}, P2 = {vr[2], zf};
-    f2v m, u;
-    PK_MUL(m, R0, P0, "op_sel:[0,0] op_sel_hi:[1,0]");             // T[3i] v0
-    PK_FMA(m, R1, P1, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+1] v1
-    PK_FMA(u, R2, P2, m, "op_sel:[0,0,0] op_sel_hi:[1,0,1]");      // + T[3i+2] v2
-    d.uvw[0] = u.x; d.uvw[1] = u.y;
-    // ground_speed's (v.r, r.r) = fma(., z, fma(., x, . y)) per half
-    PK_MUL(m, P1, P1, "op_sel:[0,1] op_sel_hi:[1,1]");             // (vy ry, ry ry)
-    PK_FMA(m, P0, P0, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vx rx, rx rx)
-    PK_FMA(m, P2, P2, m, "op_sel:[0,1,0] op_sel_hi:[1,1,1]");      // + (vz rz, rz rz)
-    const float vv = vr[0] * vr[0] + vr[1] * vr[1] + vr[2] * vr[2];
-    d.vg = __builtin_amdgcn_sqrtf(fmaxf(vv - m.x * m.x * __builtin_amdgcn_rcpf(m.y), 0.0f));
-  }
   // J2 gravity (FGInertial::GetGravityJ2), ECEF
   const float adivr = (float)WGS_A * inv_r;
   const float pre = 1.5f * (float)J2_E * adivr * adivr;
@@ -1380,7 +1354,7 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
   }
   F16_STAMP(stamps, ST_PROP);
   Derived d;
-  derive<!LOWREG>(L, ce, se, A, d);
+  derive(L, ce, se, A, d);
   F16_STAMP(stamps, ST_DERIVE);
   // -- Auxiliary, wind-axis part (needs no atmosphere) --
   float wb[3] = {0.0f, 0.0f, 0.0f};
