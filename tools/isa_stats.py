@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Static ISA statistics of the step kernel (cross-compiled here, no GPU needed).
 
-    python tools/isa_stats.py [-DFLAG ...] [--kernel _Z15f16_step_kernel8StepArgs] [--dump out.s]
+    python tools/isa_stats.py [-DFLAG ...] [--kernel MANGLED_NAME] [--dump out.s]
+
+(default kernel: the bench headline's f16_step_win_nt_kernel<0, 1, false>)
 
 Prints the kernel's VGPR/AGPR/SGPR-spill counts, the VALU / VMEM / LDS / SALU instruction
 counts of the whole kernel and of each loop (the FDM frame loop dominates: it runs
@@ -42,7 +44,7 @@ def main():
     for a in sys.argv[1:]:
         if a.startswith("-mllvm="):
             flags += ["-mllvm", a[len("-mllvm="):]]
-    kernel = "_Z15f16_step_kernel8StepArgs"
+    kernel = "_Z22f16_step_win_nt_kernelILi0ELi1ELb0EEvPK15HIP_vector_typeIfLj4EEPKfS3_l8StepArgs"
     dump = None
     args = [a for a in sys.argv[1:] if not a.startswith(("-D", "-f", "-mllvm="))]
     for i, a in enumerate(args):
