@@ -636,7 +636,8 @@ def fused_step_legs(envs, act, s, e, iters):
     handle, whose plain step keeps the feature window in its epilogue (f16env_window_step_ex,
     F16_STEP_FEATURE_WINDOW), step + features per step against the plain
     step; (2) the plain step with its actions drawn in the kernel (step(None, seed, step):
-    no sampling launch, no action read; item 5) against sample_actions + step. Host-driven
+    no sampling launch, no action read; item 5) against sample_actions + step; (3) a fused_poses
+    handle (the render/telemetry pose export in the epilogue) against step + f16env_poses. Host-driven
     loops timed by HIP events on the launch stream (the region) and the kernels' own dispatch
     events (profile_kernel)."""
     import torch
@@ -677,6 +678,23 @@ def fused_step_legs(envs, act, s, e, iters):
     out["in_kernel_actions_step_ms"] = round(in_kernel, 5)
     out["in_kernel_actions_kernel_ms"] = round(ik, 5)
     out["in_kernel_actions_kernel"] = lib_name(envs, 0)
+    # (3) the pose export in the step's epilogue (fused_poses, F16_STEP_POSES, ABI 5) against the
+    # plain step followed by the separate pose kernel (telemetry.poses of the newest frame)
+    from f16_jsb_amd.abi import F16_STEP_POSES
+    from f16_jsb_amd.telemetry import poses as _poses
+    fp = F16Envs(envs.n, stack_k=envs.k, seed=1, obs_layout="window", fused_poses=True)
+    fp.reset()
+    pbuf = torch.empty((envs.n, 10), dtype=torch.float32, device=act.device)
+    for _ in range(4):
+        fp.step(act)
+    fused_p = region(lambda t: fp.step(act))
+    fpk, _, _ = fp.profile_kernel(lambda: [fp.step(act) for _ in range(n2)], n2)
+    step_then_poses = region(lambda t: (envs.step(act), _poses(envs.obs, pbuf)))
+    out["fused_poses_step_ms"] = round(fused_p, 5)
+    out["fused_poses_kernel_ms"] = round(fpk, 5)
+    out["fused_poses_kernel"] = lib_name(fp, F16_STEP_POSES)
+    out["step_then_poses_ms"] = round(step_then_poses, 5)
+    fp.close()
     return out
 
 

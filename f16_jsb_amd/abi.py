@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 
-F16ENV_ABI_VERSION = 4  # include/f16env.h (checked against f16env_abi_version() at load)
+F16ENV_ABI_VERSION = 5  # include/f16env.h (checked against f16env_abi_version() at load)
 F16_OBS_DIM = 15
 F16_ACT_DIM = 4
 
@@ -141,6 +141,7 @@ def algorithmic_bytes_per_env_step(stack_k: int, state_bytes: int, layout: str =
 F16_SLOT_CLIP = 0x1  # the env steps np.clip(act, low, high); the slot keeps act unclipped
 F16_SLOT_FEATURE_WINDOW = 0x2  # the windowed rollout-slot step also updates the bound feature histories
 F16_STEP_FEATURE_WINDOW = 0x2  # f16env_window_step_ex: the plain windowed step updates them too (ABI 4)
+F16_STEP_POSES = 0x4  # f16env_window_step_ex: the step writes the bound N x 10 pose export (ABI 5)
 
 
 class RolloutSlot(ctypes.Structure):

@@ -557,6 +557,41 @@ __device__ __forceinline__ void stage_tables(float* sT) {
   __syncthreads();
 }
 
+// Render/telemetry pose of one observation frame x: what JSBSimEnv.render
+// (jsbsim_gym/jsbsim_gym.py:381-415) hands the Viewer -- the aircraft position in viewer axes
+// (-y, h, x) * 1e-3, its attitude Quaternion.from_euler(phi, theta, psi) (visualization/
+// quaternion.py:38-45, q_psi * q_theta * q_phi) remapped (w, -y, -z, x), and the goal position
+// in viewer axes -- in float32 with the reference's operation order (no contraction). Shared
+// by f16_poses_kernel and the plain step's epilogue (F16_STEP_POSES), so both give the same bits.
+__device__ __forceinline__ void quat_mul_ref(const float* a, const float* b, float* o) {
+#pragma clang fp contract(off)
+  // quaternion.py:11-14: w = a0 b0 - a.b ; v = a0 b + b0 a + a x b  (float32, left to right)
+  const float dot = a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+  o[0] = a[0] * b[0] - dot;
+  const float cx = a[2] * b[3] - a[3] * b[2], cy = a[3] * b[1] - a[1] * b[3], cz = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[0] * b[1] + b[0] * a[1] + cx;
+  o[2] = a[0] * b[2] + b[0] * a[2] + cy;
+  o[3] = a[0] * b[3] + b[0] * a[3] + cz;
+}
+__device__ __forceinline__ void pose_of_frame(const float* x, float* o) {
+#pragma clang fp contract(off)
+  const float s = 1e-3f;
+  o[0] = -x[1] * s; o[1] = x[2] * s; o[2] = x[0] * s;
+  const float hp = x[9] / 2.0f, ht = x[10] / 2.0f, hs = x[11] / 2.0f;
+  float sp, cp, st, ct, ss, cs;
+  sincosf(hp, &sp, &cp);
+  sincosf(ht, &st, &ct);
+  sincosf(hs, &ss, &cs);
+  const float q1[4] = {cp, sp, 0.0f, 0.0f};
+  const float q2[4] = {ct, 0.0f, st, 0.0f};
+  const float q3[4] = {cs, 0.0f, 0.0f, ss};
+  float q32[4], q[4];
+  quat_mul_ref(q3, q2, q32);
+  quat_mul_ref(q32, q1, q);
+  o[3] = q[0]; o[4] = -q[2]; o[5] = -q[3]; o[6] = q[1];
+  o[7] = -x[13] * s; o[8] = x[14] * s; o[9] = x[12] * s;
+}
+
 struct StepArgs {
   SoA s, tmpl;
   const float* act;
@@ -601,6 +636,9 @@ struct StepArgs {
   SoA icc;
   EnvArgs E;
   ModelConsts C;
+  // the plain step's pose export (f16env_window_step_ex with F16_STEP_POSES): N x 10 floats, the
+  // pose of the returned observation's newest frame per env; nullptr: none
+  float* poses;
 };
 
 #ifdef F16_STAMPS
@@ -660,8 +698,9 @@ struct StepPre {
 // XV (windowed plain-step extras, f16_step_winx_kernel / f16env_window_step_ex): XV_FEAT keeps the
 // bound feature histories in the step's epilogue (the rollout-slot build's F16_SLOT_FEATURE_WINDOW
 // code, without the slot); every winx build draws the actions in-kernel when act == NULL
-// (a.sample_act: the f16env_sample_actions stream). The headline instances (XV = 0) carry none of
-// this code.
+// (a.sample_act: the f16env_sample_actions stream) and writes the pose export when a.poses is set
+// (F16_STEP_POSES, a run-time choice: no further instances). The headline instances (XV = 0)
+// carry none of this code.
 enum { XV_X = 1, XV_FEAT = 2 };
 template <int MODE, bool GT = false, bool ROLL = false, bool LOWREG = false, bool WIN = false, bool NT = false,
           bool HALF = false, int XV = 0>
@@ -1061,6 +1100,31 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
             if (r > p - K + 1) a.fwy[(int64_t)r * rowN + k * FEAT_OUT + j] = y[j];
           }
         }
+      }
+    }
+    if ((XV & XV_X) != 0 && a.poses) {
+      // the pose export (F16_STEP_POSES, f16_poses_kernel's output written here instead of by a
+      // second launch): the pose of the returned observation's newest frame; the wave's 64 rows
+      // (640 contiguous floats) leave through its staging area as float4
+      float po[10];
+      if (live) pose_of_frame(reset_now ? f0 : f, po);
+      if (rows == EPW) {
+        float* sp = stg;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 10; ++j) sp[lane * 10 + j] = po[j];
+        __builtin_amdgcn_wave_barrier();
+        float* g = a.poses + row0 * 10;
+        if (((uintptr_t)g & 15) == 0) {
+          for (int u = lane; u < 64 * 10 / 4; u += 64)
+            reinterpret_cast<float4*>(g)[u] = reinterpret_cast<const float4*>(sp)[u];
+        } else {
+          for (int u = lane; u < 64 * 10; u += 64) g[u] = sp[u];
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (live) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) a.poses[k * 10 + j] = po[j];
       }
     }
     F16_STAMP(stamps, ST_COPY);
@@ -2075,22 +2139,9 @@ __global__ __launch_bounds__(256) void f16_feature_window_kernel(FeatWinArgs a) 
   }
 }
 
-// Render/telemetry poses of one frame per env: what JSBSimEnv.render
-// (jsbsim_gym/jsbsim_gym.py:381-415) hands the Viewer -- the aircraft position in viewer axes
-// (-y, h, x) * 1e-3, its attitude Quaternion.from_euler(phi, theta, psi) (visualization/
-// quaternion.py:38-45, q_psi * q_theta * q_phi) remapped (w, -y, -z, x), and the goal position
-// in viewer axes -- in float32 with the reference's operation order. One lane per env; frames
-// are read with a caller stride so obs[:, -1, :] of a (N, K, 15) stack needs no copy.
-__device__ __forceinline__ void quat_mul_ref(const float* a, const float* b, float* o) {
-#pragma clang fp contract(off)
-  // quaternion.py:11-14: w = a0 b0 - a.b ; v = a0 b + b0 a + a x b  (float32, left to right)
-  const float dot = a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
-  o[0] = a[0] * b[0] - dot;
-  const float cx = a[2] * b[3] - a[3] * b[2], cy = a[3] * b[1] - a[1] * b[3], cz = a[1] * b[2] - a[2] * b[1];
-  o[1] = a[0] * b[1] + b[0] * a[1] + cx;
-  o[2] = a[0] * b[2] + b[0] * a[2] + cy;
-  o[3] = a[0] * b[3] + b[0] * a[3] + cz;
-}
+// Render/telemetry poses of one frame per env (pose_of_frame above). One
+// lane per env; frames are read with a caller stride so obs[:, -1, :] of a (N, K, 15) stack needs
+// no copy.
 // 256 envs per block; 16-B aligned frames (the windowed layout's 64-B slots) are read as
 // 3 x float4 + float2 + float, and the block's 256 x 10 poses leave through LDS as contiguous
 // float4 (a 40-B row per lane would be 10 partial-line dword stores)
@@ -2117,22 +2168,7 @@ __global__ __launch_bounds__(256) void f16_poses_kernel(int64_t n, const float* 
 #pragma unroll
       for (int j = 0; j < F16_OBS_DIM; ++j) x[j] = f[j];
     }
-    const float s = 1e-3f;
-    float* o = sOut + t * 10;
-    o[0] = -x[1] * s; o[1] = x[2] * s; o[2] = x[0] * s;
-    const float hp = x[9] / 2.0f, ht = x[10] / 2.0f, hs = x[11] / 2.0f;
-    float sp, cp, st, ct, ss, cs;
-    sincosf(hp, &sp, &cp);
-    sincosf(ht, &st, &ct);
-    sincosf(hs, &ss, &cs);
-    const float q1[4] = {cp, sp, 0.0f, 0.0f};
-    const float q2[4] = {ct, 0.0f, st, 0.0f};
-    const float q3[4] = {cs, 0.0f, 0.0f, ss};
-    float q32[4], q[4];
-    quat_mul_ref(q3, q2, q32);
-    quat_mul_ref(q32, q1, q);
-    o[3] = q[0]; o[4] = -q[2]; o[5] = -q[3]; o[6] = q[1];
-    o[7] = -x[13] * s; o[8] = x[14] * s; o[9] = x[12] * s;
+    pose_of_frame(x, sOut + t * 10);
   }
   __syncthreads();
   float* g = out + k0 * 10;
@@ -2166,6 +2202,7 @@ struct f16env {
   int win_half;       // experiment (F16ENV_HALF=1): 32 envs per wave, f16_step_win_half_kernel
   int half_delay;     // ... and the second half of its grid starting this many cycles late
   float* fw[2];       // f16env_window_feature_bind: the feature histories (parity 0, 1)
+  float* poses;       // f16env_window_poses_bind: N x 10 pose export of F16_STEP_POSES steps
   struct {            // f16env_window_bind: the buffers of f16env_window_step_bound
     float* hist[2];
     int64_t T;
@@ -2692,7 +2729,14 @@ static int step_window_impl(f16env_t h, void* stream, const f16env_rollout_slot*
   } else if (ex) {  // f16env_window_step_ex: the winx build (in-kernel actions, feature window)
     a.sample_act = act ? 0 : 1;
     a.act_seed = act_seed; a.act_step = act_step;
-    if (xflags & ~(uint32_t)F16_STEP_FEATURE_WINDOW) return set_err(-1, "unknown f16env_window_step_ex flags");
+    if (xflags & ~(uint32_t)(F16_STEP_FEATURE_WINDOW | F16_STEP_POSES))
+      return set_err(-1, "unknown f16env_window_step_ex flags");
+    if (xflags & F16_STEP_POSES) {
+      if (!h->poses) return set_err(-1, "F16_STEP_POSES: f16env_window_poses_bind first");
+      if (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period <= 0)
+        return set_err(-1, "F16_STEP_POSES: not with the deferred-reset step (F16ENV_ICC_PERIOD=0)");
+      a.poses = h->poses;
+    }
     if (xflags & F16_STEP_FEATURE_WINDOW) {
       if (!h->fw[0] || !h->fw[1]) return set_err(-1, "F16_STEP_FEATURE_WINDOW: f16env_window_feature_bind first");
       if (hist_cur != h->wb.hist[0] && hist_cur != h->wb.hist[1])
@@ -2795,6 +2839,13 @@ int f16env_window_feature_bind(f16env_t h, float* feat0, float* feat1) {
   if ((!feat0) != (!feat1) || (feat0 && feat0 == feat1)) return set_err(-1, "two distinct feature histories (or none)");
   if (((((uintptr_t)feat0) | ((uintptr_t)feat1)) & 3) != 0) return set_err(-1, "feature histories must be float-aligned");
   h->fw[0] = feat0; h->fw[1] = feat1;
+  return 0;
+}
+
+int f16env_window_poses_bind(f16env_t h, float* poses) {
+  if (!h) return set_err(-1, "null handle");
+  if (((uintptr_t)poses & 3) != 0) return set_err(-1, "poses must be float-aligned");
+  h->poses = poses;
   return 0;
 }
 

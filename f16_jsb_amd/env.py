@@ -23,7 +23,7 @@ from . import spaces
 from ._lib import F16EnvError, check, lib
 from .abi import (RolloutSlot, F16C_N, F16_IC_N, F16_OBS_DIM, F16_FLAG_GUSTS, F16_FLAG_NAN_GUARD, F16_FLAG_NO_AUTORESET,
                   F16_FLAG_OBS_CHECK, F16_SLOT_CLIP, F16_SLOT_FEATURE_WINDOW, F16_STEP_FEATURE_WINDOW,
-                  F16_FLAG_RANDOM_IC,
+                  F16_STEP_POSES, F16_FLAG_RANDOM_IC,
                   EnvConfig, algorithmic_bytes_per_env_step, config_default)
 
 StepOut = namedtuple("StepOut", "obs rew terminated truncated terminal_obs ep_return ep_len")
@@ -59,7 +59,8 @@ class F16Envs:
                  env_id_base: int = 0, max_steps: int = 1200, down_sample: int = 4,
                  autoreset: bool = True, ic=None, nan_guard: bool = False, obs_check: bool = False,
                  obs_layout: str = "contiguous",
-                 history: int = 0, window_order: str = "position", fused_features: bool = False, **cfg_kw):
+                 history: int = 0, window_order: str = "position", fused_features: bool = False,
+                 fused_poses: bool = False, **cfg_kw):
         """obs_layout "contiguous": observations in two ping-pong (N, K, 15) buffers (f16env_step).
         obs_layout "window": observations are (N, K, 15) views of two per-env frame histories of
         `history` positions of 64-B frame slots, position-major [T][N][16] (f16env_step_window:
@@ -73,7 +74,10 @@ class F16Envs:
         windows (obs_features(), features.py:37-67 per frame) in its own epilogue -- the step's
         feature-window build (f16env_window_step_ex, F16_STEP_FEATURE_WINDOW), no second launch;
         obs_features() is then a view. Off by default: the plain step's instance carries none of
-        that code."""
+        that code.
+        fused_poses (windowed layout): every step also writes the render/telemetry pose of the
+        returned observation's newest frame (poses(), telemetry.poses of obs[:, -1], the same
+        bits) in its epilogue (f16env_window_step_ex, F16_STEP_POSES): no second launch."""
         import torch
 
         if not torch.cuda.is_available():
@@ -126,10 +130,13 @@ class F16Envs:
             self._feat_prev_ok = False  # the feature windows hold the last step's ahead fills
             self.feature_window_calls = {"incremental": 0, "full": 0, "fused": 0}
         else:
-            if fused_features:
-                raise ValueError("fused_features needs obs_layout='window'")
+            if fused_features or fused_poses:
+                raise ValueError("fused_features / fused_poses need obs_layout='window'")
             self._obs = [torch.zeros((n, k, F16_OBS_DIM), dtype=f32, device=dev) for _ in range(2)]
         self.fused_features = bool(fused_features)
+        self.fused_poses = bool(fused_poses)
+        self._poses = None    # (N, 10) pose export; _poses_op: the op it describes
+        self._poses_op = -1
         self._cur = 0
         # rewards (f32), terminated, truncated (u8) in ONE allocation, so a host-side consumer
         # (F16VecEnv's numpy mode) moves the three with a single device-to-host copy
@@ -155,6 +162,9 @@ class F16Envs:
             self.terminal_obs = self._window(1)
             if self.fused_features:
                 self._feature_hist()
+            if self.fused_poses:
+                self._poses = torch.zeros((n, 10), dtype=f32, device=dev)
+                check(L.f16env_window_poses_bind(self._h, self._poses.data_ptr()), "f16env_window_poses_bind")
         else:
             self._obs_ptr = [o.data_ptr() for o in self._obs]
             self._out_ptr = (self.rew.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr(),
@@ -278,7 +288,7 @@ class F16Envs:
         if features is not None:
             return self.step_rollout(0, 0, features=features, policy_actions=actions)
         if self.window:
-            if self.fused_features and done_idx is None and n_done is None:
+            if (self.fused_features or self.fused_poses) and done_idx is None and n_done is None:
                 return self._step_window_ex(self._as_act(actions), 0, 0)
             return self._step_window(actions, done_idx, n_done)
         t = self.torch
@@ -331,10 +341,12 @@ class F16Envs:
         whenever they are current before it, and catches them up after a step that could not."""
         fw = self.fused_features and self._fh is not None and self._feat_prev_ok and self._feat_op == self._op
         s, cur, p = self._advance()
+        flags = (F16_STEP_FEATURE_WINDOW if fw else 0) | (F16_STEP_POSES if self.fused_poses else 0)
         check(self._step_ex(self._h, s, None if act is None else act.data_ptr(), cur, p,
-                            F16_STEP_FEATURE_WINDOW if fw else 0, seed & 0xFFFFFFFFFFFFFFFF,
-                            step & 0xFFFFFFFFFFFFFFFF), "f16env_window_step_ex")
+                            flags, seed & 0xFFFFFFFFFFFFFFFF, step & 0xFFFFFFFFFFFFFFFF), "f16env_window_step_ex")
         out = self._fused_done(fw, self._advanced(cur, p))
+        if self.fused_poses:
+            self._poses_op = self._op
         if self.fused_features and not fw:
             self.obs_features()  # whole windows + the step's ahead fills: the next step fuses
         return out
@@ -575,6 +587,20 @@ class F16Envs:
             self._op += 1
         else:
             self._obs[self._cur].copy_(o)
+
+    def poses(self):
+        """(N, 10) float32 render/telemetry poses of the current observation's newest frame
+        (telemetry.poses(self.obs[:, -1]), JSBSimEnv.render, jsbsim_gym.py:381-415). A
+        fused_poses handle's step writes them in its epilogue, so after such a step this is the
+        bound buffer with no launch; otherwise (or after any other op) f16env_poses computes them.
+        The result is a view valid until the next op."""
+        from .telemetry import poses as _poses
+        if self._poses is not None and self._poses_op == getattr(self, "_op", None):
+            return self._poses
+        out = _poses(self.obs, out=self._poses)  # (the newest frame of each stack, read in place)
+        if self._poses is not None:
+            self._poses_op = getattr(self, "_op", None)
+        return out
 
     def obs_features(self):
         """(N, K, 17) float32 policy features of the current observation (features.py:37-67 per

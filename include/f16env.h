@@ -51,8 +51,9 @@ extern "C" {
  * f16env_bootstrap_apply, f16env_features_window_step, f16env_window_feature_bind
  * (+ F16_SLOT_FEATURE_WINDOW), f16env_abi_version.
  * 4 (round 5): new f16env_window_step_ex (in-step action draws, F16_STEP_FEATURE_WINDOW) and
- * f16env_window_step_ex_kernel_name; nothing else changed. */
-#define F16ENV_ABI_VERSION 4
+ * f16env_window_step_ex_kernel_name; nothing else changed.
+ * 5 (round 5): new F16_STEP_POSES flag and f16env_window_poses_bind; nothing else changed. */
+#define F16ENV_ABI_VERSION 5
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
 #define F16_OBS_DIM 15
@@ -268,8 +269,17 @@ int f16env_window_feature_bind(f16env_t h, float* feat0, float* feat1);
  *                registers: no second launch), exactly as F16_SLOT_FEATURE_WINDOW does in a
  *                rollout-slot step; same precondition (both feature windows current before the
  *                step). Refused with the deferred-reset step (F16ENV_ICC_PERIOD=0).
+ *   flags F16_STEP_POSES (ABI 5)  the step also writes the render/telemetry pose of the returned
+ *                observation's newest frame per env into the N x 10 buffer bound by
+ *                f16env_window_poses_bind -- f16env_poses of that frame (JSBSimEnv.render,
+ *                jsbsim_gym.py:381-415), the same bits, without the second launch. Refused with
+ *                the deferred-reset step (F16ENV_ICC_PERIOD=0).
  * With act != NULL and flags 0 it is f16env_window_step_bound. */
 #define F16_STEP_FEATURE_WINDOW 0x2
+#define F16_STEP_POSES 0x4
+/* The N x 10 float32 pose buffer F16_STEP_POSES steps write (16-B aligned for whole-line stores;
+ * NULL: unbind). Replaces nothing in the reference (a render callback's input, see f16env_poses). */
+int f16env_window_poses_bind(f16env_t h, float* poses);
 int f16env_window_step_ex(f16env_t h, void* stream, const float* act, int32_t parity, int32_t pos, uint32_t flags,
                           uint64_t act_seed, uint64_t act_step);
 /* The kernel instance f16env_window_step_ex launches for `flags` (as rocprofv3 demangles it). */
