@@ -53,9 +53,11 @@ for s in $STEPS; do
     smoke) run smoke_$TAG 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 50 ;;
     driver) run bench_driver_$TAG 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    profdrv)  # rocprofv3 summary of the driver's exact command
+    profdrv)  # rocprofv3 summary of the driver's exact command (the per-dispatch trace is dropped:
+              # gpurun copies back at most 64 MiB of gpurun_out)
       (cd /tmp && run_abs prof_drv_$TAG 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/prof_drv_$TAG" -o run --output-format csv -- \
-        python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5) || exit $? ;;
+        python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5) || exit $?
+      rm -f "$OUT/prof_drv_$TAG/run_kernel_trace.csv" ;;
     dist2)  # the bench's N > 1 code path with 2 ranks sharing this box's GPU (gloo: rehearsal only)
       run bench_dist2_$TAG 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo ;;
@@ -87,14 +89,18 @@ for s in $STEPS; do
     report) run parity_report 600 python tests/parity_report.py --n 256 --steps 300 --json "$OUT/parity_$TAG.json" ;;
     prof)
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \
-        python bench.py --steps 300 --warmup 20 --no-cpu-baseline --rollout-envs 0 ;;
-    sq)  # summary: python tools/pmc_valu.py gpurun_out/pmc_sq*_$TAG --out profiles/pmc_valu.json
+        python bench.py --steps 300 --warmup 20 --no-cpu-baseline --rollout-envs 0
+      rm -f "$OUT/prof_$TAG/run_kernel_trace.csv" ;;
+    sq)  # summarised on the box (pmc_valu_$TAG.json), the raw rows compressed
       run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_sq_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_sq3 600 rocprofv3 --pmc SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 -d "$OUT/pmc_sq3_$TAG" -o run --output-format csv -- \
-        python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0 ;;
+        python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
+      python tools/pmc_valu.py "$OUT/pmc_sq_$TAG" "$OUT/pmc_sq2_$TAG" "$OUT/pmc_sq3_$TAG" --kernel f16_step_win_nt_kernel \
+        --out "$OUT/pmc_valu_$TAG.json" > /dev/null
+      for d in pmc_sq_$TAG pmc_sq2_$TAG pmc_sq3_$TAG; do tar cJf "$OUT/$d.tar.xz" -C "$OUT" $d && rm -rf "$OUT/$d"; done ;;
     pmc5)  # HBM traffic of the cfg5 step kernel (summary: tools/pmc_traffic.py ... --envs 131072 --extra-bytes 24)
       run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc5_fetch_$TAG" -o run --output-format csv -- \
         python bench.py --workload cfg5 --steps 50 --warmup 5 --no-cpu-baseline
@@ -104,7 +110,10 @@ for s in $STEPS; do
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- \
         python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o run --output-format csv -- \
-        python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0 ;;
+        python bench.py --steps 50 --warmup 5 --no-cpu-baseline --rollout-envs 0
+      python tools/pmc_traffic.py "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" --envs 65536 --stack 4 \
+        --kernel f16_step_win_nt_kernel --out "$OUT/pmc_traffic_$TAG.json" > /dev/null
+      for d in pmc_fetch_$TAG pmc_write_$TAG; do tar cJf "$OUT/$d.tar.xz" -C "$OUT" $d && rm -rf "$OUT/$d"; done ;;
   esac
 done
 echo "[session] done"
