@@ -47,9 +47,10 @@ def poses(obs: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
 
 def snapshot(envs, path: str = None):
     """Poses of every env of an F16Envs handle as a host numpy array (and optionally a .npy
-    file): the telemetry record a viewer replays."""
+    file): the telemetry record a viewer replays. (envs.poses(): a fused_poses handle's step has
+    already written them, no launch here.)"""
     import numpy as np
-    p = poses(envs.obs).cpu().numpy()
+    p = (envs.poses() if hasattr(envs, "poses") else poses(envs.obs)).cpu().numpy()
     if path is not None:
         np.save(path, p)
     return p
