@@ -180,12 +180,14 @@ static constexpr float RAD2DEG_F = 57.295779513082320876798f;
 // epilogue store tail). fp64 fields occupy two lanes of a column.
 //   C0  rI.x rI.y (f64)        C6  aI.z aIp.xyz           C12 pid_p_i pid_y_i pid_y_p n2'
 //   C1  rI.z vI.x (f64)        C7  q0 q1 q2 q3            C13 alpha beta mach qc      (latch)
-//   C2  vI.y vI.z (f64)        C8  wI.xyz wId.x           C14 npy npz goal.x goal.y   (latch, goal)
-//   C3  epa ep_ret (f64)       C9  wId.yz ba.y ba.z       C15 goal.z last_d' step ep_count (i32)
+//   C2  vI.y vI.z (f64)        C8  wI.xyz wId.x           C14 last_d' step (i32) npy npz
+//   C3  epa ep_ret (f64)       C9  wId.yz ba.y ba.z       C15 goal.xyz ep_count (i32) (per episode)
 //   C4  ndv1.xyz dv2.x         C10 tef ail ele rud        C16 steady wind.xyz, 0  (wind kernels only)
 //   C5  dv2.yz aI.xy           C11 lef sb pid_r_i pid_r_p C17 gust.xyz, 0         (wind kernels only)
 // n2' = N2 with the augmentation flag in its sign bit (N2 >= 60 %), last_d' = last distance
-// with the FRESH flag in its sign bit (a norm, >= 0). Not stored, because a step never reads
+// with the FRESH flag in its sign bit (a norm, >= 0). C15 changes only when the lane resets, so
+// the step stores it for the lanes it reset and no others (round 5: 16 B of the 256 per env
+// step not written back). Not stored, because a step never reads
 // them from the previous one: the latch's body rates wrt ECEF (p/q/r-aero = wI - Ti2b (0, 0,
 // w_earth), a function of q and wI) and ground speed (a function of rI, vI), recomputed at load
 // (latch_from_state) exactly as a frame computes them (the last frame of a step runs after the
@@ -309,10 +311,10 @@ __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, f
   L.ppi = c[12].x; L.pyi = c[12].y; L.pyp = c[12].z; L.ppp = 0.0f;
   L.n2 = without_sign_flag(c[12].w); L.n1 = 0.0f;
   L.lx[F16L_ALPHA] = c[13].x; L.lx[F16L_BETA] = c[13].y; L.lx[F16L_MACH] = c[13].z; L.lx[F16L_VC_KTS] = c[13].w;
-  L.lx[F16L_NPY] = c[14].x; L.lx[F16L_NPZ] = c[14].y; L.goal[0] = c[14].z; L.goal[1] = c[14].w;
-  L.goal[2] = c[15].x; L.last_d = without_sign_flag(c[15].y);
-  L.step = __float_as_int(c[15].z); L.ep_count = __float_as_int(c[15].w);
-  L.flags = (sign_flag(c[12].w) ? LANE_FLAG_AUG : 0) | (sign_flag(c[15].y) ? LANE_FLAG_FRESH : 0);
+  L.last_d = without_sign_flag(c[14].x); L.step = __float_as_int(c[14].y);
+  L.lx[F16L_NPY] = c[14].z; L.lx[F16L_NPZ] = c[14].w;
+  L.goal[0] = c[15].x; L.goal[1] = c[15].y; L.goal[2] = c[15].z; L.ep_count = __float_as_int(c[15].w);
+  L.flags = (sign_flag(c[12].w) ? LANE_FLAG_AUG : 0) | (sign_flag(c[14].x) ? LANE_FLAG_FRESH : 0);
   latch_from_state(L);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -347,10 +349,12 @@ __device__ __forceinline__ void lane_load_lds(const float4* cols, Lane& L) {
   lane_unpack<false>(c, z, z, L);
 }
 
-// PART: 0 every column; 1 the columns a step's frames leave final (all but C3 and C15, which
-// the env layer still changes: episode return, last distance, and a reset); 2 C3 and C15.
+// PART: 0 every column; 1 the columns a step's frames leave final (all but C3, C14 and C15,
+// which the env layer still changes: episode return, last distance, a reset); 2 C3, C14 and C15.
+// with15 false: C15 (goal, episode count) is left as it is in memory -- a step whose lane did not
+// reset has not changed it.
 template <bool GUST = false, int PART = 0, bool NT = false>
-__device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L) {
+__device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& L, bool with15 = true) {
   const int64_t n = s.n;
   float4 c[NCOL];
   c[0] = make_float4(dlo(L.rI[0]), dhi(L.rI[0]), dlo(L.rI[1]), dhi(L.rI[1]));
@@ -367,13 +371,14 @@ __device__ __forceinline__ void lane_store(const SoA& s, int64_t k, const Lane& 
   c[11] = make_float4(L.lef, L.sb, L.pri, L.prp);
   c[12] = make_float4(L.ppi, L.pyi, L.pyp, with_sign_flag(L.n2, (L.flags & LANE_FLAG_AUG) != 0));
   c[13] = make_float4(L.lx[F16L_ALPHA], L.lx[F16L_BETA], L.lx[F16L_MACH], L.lx[F16L_VC_KTS]);
-  c[14] = make_float4(L.lx[F16L_NPY], L.lx[F16L_NPZ], L.goal[0], L.goal[1]);
-  c[15] = make_float4(L.goal[2], with_sign_flag(L.last_d, (L.flags & LANE_FLAG_FRESH) != 0),
-                      __int_as_float(L.step), __int_as_float(L.ep_count));
+  c[14] = make_float4(with_sign_flag(L.last_d, (L.flags & LANE_FLAG_FRESH) != 0), __int_as_float(L.step),
+                      L.lx[F16L_NPY], L.lx[F16L_NPZ]);
+  c[15] = make_float4(L.goal[0], L.goal[1], L.goal[2], __int_as_float(L.ep_count));
   float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n)
-    if (PART == 0 || (PART == 1) == (j != 3 && j != 15)) st16<NT>(p, c[j]);
+    if (PART == 0 || (PART == 1) == (j != 3 && j != 14 && j != 15))
+      if (j != 15 || with15) st16<NT>(p, c[j]);
   if (GUST && PART != 2) {
     st16<NT>(p, make_float4(L.wst[0], L.wst[1], L.wst[2], 0.0f));
     st16<NT>(p + n, make_float4(L.gust[0], L.gust[1], L.gust[2], 0.0f));

@@ -19,6 +19,9 @@
 
 #include "../../include/f16env.h"
 #include "f16_device.h"
+#ifndef F16_C15_ALWAYS
+#define F16_C15_ALWAYS 0
+#endif
 
 using namespace f16;
 
@@ -927,10 +930,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       }
     }
     F16_STAMP(stamps, ST_RESET);
-    if (!early_store || (done && (!DEFER || in_step_reset) && !(a.E.flags & F16_FLAG_NO_AUTORESET)))
-      lane_store<GUST, 0, NT>(a.s, k, L);    // every column (a lane reset just now rewrites its row)
+    // C15 (goal, episode count) changes only in a reset: written back for the lanes reset here
+    // (F16_C15_ALWAYS=1: every lane, the A/B reference)
+    const bool reset_here = done && (!DEFER || in_step_reset) && !(a.E.flags & F16_FLAG_NO_AUTORESET);
+    if (!early_store || reset_here)
+      lane_store<GUST, 0, NT>(a.s, k, L, F16_C15_ALWAYS || reset_here);  // every column (a lane reset just now rewrites its row)
     else
-      lane_store<GUST, 2, NT>(a.s, k, L);  // the rest
+      lane_store<GUST, 2, NT>(a.s, k, L, false);  // the rest
     F16_STAMP(stamps, ST_STORE);
   }
   sDone[threadIdx.x] = done;
@@ -1767,7 +1773,7 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int*
   // handle's observation histories, not the physics state, so it survives a set_state: a
   // reset -> set_state -> step sequence still fills the new window from the reset frame
   // (f16env_window_clear_fresh drops it once the caller has written whole windows)
-  const bool fresh = sign_flag(s.c[(int64_t)15 * s.n + k].y);
+  const bool fresh = sign_flag(s.c[(int64_t)14 * s.n + k].x);
   L.flags = (o[F16C_AUG] != 0.0 ? LANE_FLAG_AUG : 0) | (fresh ? LANE_FLAG_FRESH : 0);
   for (int j = 0; j < F16L_N; ++j) L.lx[j] = (float)o[F16C_LX + j];
   L.lx[F16L_VC_KTS] = qc_from_vcas(o[F16C_LX + F16L_VC_KTS], C);
@@ -1781,11 +1787,11 @@ __global__ void f16_set_state_kernel(SoA s, const double* c, ModelConsts C, int*
 }
 
 // the caller wrote whole observation windows into both histories (F16Envs.set_obs): no lane
-// needs its window filled from a reset frame any more (the FRESH sign bit of column 15's y)
+// needs its window filled from a reset frame any more (the FRESH sign bit of column 14's x)
 __global__ void f16_clear_fresh_kernel(SoA s) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= s.n) return;
-  float* y = &s.c[(int64_t)15 * s.n + k].y;
+  float* y = &s.c[(int64_t)14 * s.n + k].x;
   *y = without_sign_flag(*y);
 }
 
