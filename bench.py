@@ -1139,7 +1139,8 @@ def main():
             "region_ms_per_launch": round(gpu_ms_per_step, 5),
             "region_timing": "HIP events around the timed region on the launch stream / launches",
             "algorithmic_bytes_per_env_step": bytes_per_env_step,
-            "bytes_basis": ("%s layout: 16 (action) + 2 x 60 (new frame into both histories) + 4 + 2 + 2S, S = %d"
+            "bytes_basis": ("%s layout: 16 (action) + 2 x 60 (new frame into both histories) + 4 + 2 + S + (S - 16) "
+                            "(the per-episode state column is written back only by lanes the step reset), S = %d"
                             % (args.obs_layout, envs.state_bytes_per_env) if envs.window else
                             "SURVEY 8(d) B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S, S = %d" % envs.state_bytes_per_env),
             # SURVEY 8(d)'s B(K), the bytes of the same step with the K-frame stack materialised

@@ -129,10 +129,13 @@ def algorithmic_bytes_per_env_step(stack_k: int, state_bytes: int, layout: str =
     """Bytes one env step must move. Contiguous stacks, SURVEY.md 8(d):
     B(K) = 16 + 60K + 60(K-1) + 4 + 2 + 2S (action, the new stack written, the previous K-1
     frames read, reward, flags, state read + written). Windowed observations
-    (f16env_step_window): B_win = 16 + 2*60 + 4 + 2 + 2S, independent of K -- the new frame
-    written to both histories, no frames read (a reset lane's fresh window aside)."""
+    (f16env_step_window): B_win = 16 + 2*60 + 4 + 2 + S + (S - 16), independent of K -- the
+    new frame written to both histories, no frames read (a reset lane's fresh window aside), the
+    state read whole and written back without its per-episode column (goal, episode count),
+    which only a lane the step resets rewrites (round 5; ~0.1 % of lanes per step in the bench's
+    steady state)."""
     if layout == "window":
-        return 16 + 2 * 60 + 4 + 2 + 2 * state_bytes
+        return 16 + 2 * 60 + 4 + 2 + 2 * state_bytes - 16
     if layout != "contiguous":
         raise ValueError("layout must be 'contiguous' or 'window'")
     return 16 + 60 * stack_k + 60 * (stack_k - 1) + 4 + 2 + 2 * state_bytes
