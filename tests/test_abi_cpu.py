@@ -45,6 +45,12 @@ def test_library_loads_without_gpu(so_path):
     s = L.f16env_state_bytes_per_env()
     assert 200 <= s <= 400
     assert L.f16env_algorithmic_bytes_per_env_step(4) == 16 + 60 * 4 + 60 * 3 + 4 + 2 + 2 * s
+    # the windowed step's moved bytes (bench.py's roofline basis): the state read whole, written
+    # back without its per-episode column (goal, episode count) except by the lanes it reset
+    from f16_jsb_amd.abi import algorithmic_bytes_per_env_step
+    assert algorithmic_bytes_per_env_step(4, s, "window") == 16 + 2 * 60 + 4 + 2 + s + (s - 16)
+    assert algorithmic_bytes_per_env_step(10, 256, "window") == 638
+    assert algorithmic_bytes_per_env_step(4, 256) == 954  # SURVEY 8(d)'s B(4), the contract
 
 
 def test_config_default_matches_python_mirror(so_path):
