@@ -19,7 +19,8 @@ Prints ONE JSON line on rank 0 (driver contract), including
                   duration (HIP events on the launch stream), vs the 8 TB/s HBM peak;
                   `traffic` = PMC-measured HBM bytes per launch from profiles/ if present;
   cpu_baseline -- the CPU oracle (oracle/f16ref.c, fp64 C restatement, OpenMP) timed on this
-                  host on a bounded sample of the same workload (rank 0, N=1 only).
+                  host on a bounded sample of the same workload (rank 0, at every N, after the
+                  closing barrier); rccl_world -- the size of the group RCCL reports.
 """
 from __future__ import annotations
 
@@ -84,13 +85,12 @@ def launch_ranks(args, argv):
     127.0.0.1) and relay rank 0's JSON line. This process makes no GPU call (torch is not even
     imported here) and never exec's: it waits for the launcher, forwards the ranks' other
     output to stderr as it arrives, and exits non-zero when any rank failed or no line came."""
-    import socket
     import subprocess
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    # --standalone: the launcher's own c10d store binds a free port itself and keeps it (a port
+    # probed here and handed over could be taken by another process in between, ADVICE r05);
+    # --local-addr keeps the rendezvous on 127.0.0.1 (the container hostname may not resolve)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", "--nproc-per-node", str(args.gpus), os.path.abspath(__file__), *argv]
     print("[bench] launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
     line = None
@@ -125,10 +125,29 @@ def launch_selftest(args, world, rank):
     dist.barrier()
     envs = args.envs or 65536
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "selftest": True,
-                          "ranks_joined": int(t.item()),
-                          "config": {"envs_per_gpu": envs, "global_envs": envs * world}}), flush=True)
+        line = {"metric": METRIC, "value": None, "n_gpus": world, "selftest": True,
+                "ranks_joined": int(t.item()),
+                "config": {"envs_per_gpu": envs, "global_envs": envs * world}}
+        # the closing fields every line carries at every N, made by the same code as the real run
+        line.update(closing_fields(args, world, min(envs, 4096), args.stack))
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
+
+
+def closing_fields(args, world, n, stack, cfg5=False, leg=None):
+    """The fields every result line carries at every N, made on rank 0 after
+    the closing barrier, when no rank is timing anything: the process group as the collective
+    library reports it (`rccl_world`: dist.get_world_size() of the nccl = RCCL group; None under
+    gloo or without a group) and the CPU baseline."""
+    import torch.distributed as dist
+    pg = {"backend": None, "world_size": 1}
+    if dist.is_available() and dist.is_initialized():
+        pg = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size()}
+    out = {"process_group": pg, "rccl_world": pg["world_size"] if pg["backend"] == "nccl" else None}
+    if not args.no_cpu_baseline:
+        run = leg or (lambda name, fn, *a: fn(*a))
+        out["cpu_baseline"] = run("cpu_baseline", cpu_baseline, n, stack, args.cpu_seconds, cfg5)
+    return out
 
 
 def cpu_baseline(envs, stack, seconds, cfg5=False):
@@ -1063,6 +1082,10 @@ def main():
         rollout = leg("rollout", rollout_bench, args, dev, rank, world)
     cfg1 = leg("cfg1_hip", cfg1_hip_bench, dev) if one else None
 
+    if world > 1:
+        # closing barrier: every rank's GPU legs are done before rank 0 samples the CPU baseline,
+        # so no timed region of any rank overlaps it
+        dist.barrier()
     if rank != 0:
         dist.destroy_process_group()
         if legs_failed:
@@ -1172,8 +1195,9 @@ def main():
         out["layouts"] = {args.obs_layout: {"kernel": kernel_name, "kernel_ms": round(kern_ms, 5),
                                             "region_ms_per_step": round(gpu_ms_per_step, 5)},
                           other: layouts}
-    if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, n, args.stack, args.cpu_seconds, cfg5)
+    # at every N: the process group RCCL reports and the CPU baseline (rank 0, after the closing
+    # barrier above)
+    out.update(closing_fields(args, world, n, args.stack, cfg5, leg))
     out["legs_failed"] = legs_failed
     print(json.dumps(out), flush=True)
     if world > 1:

@@ -20,17 +20,23 @@ def _run(args, env=None, timeout=240):
 
 
 def test_gpus2_spawns_two_ranks_and_relays_rank0_line():
-    p = _run(["--gpus", "2", "--launch-selftest"])
+    p = _run(["--gpus", "2", "--launch-selftest", "--cpu-seconds", "0.3"])
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout  # exactly the relayed line on stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks_joined"] == 2
     assert d["config"]["global_envs"] == 2 * 65536
+    # the N > 1 line carries the CPU baseline and the group's world size
+    # (rccl_world is the nccl group's size; this rehearsal's group is gloo, so it reads None)
+    assert "rccl_world" in d and d["rccl_world"] is None
+    assert d["process_group"] == {"backend": "gloo", "world_size": 2}
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1, cb
 
 
 def test_gpus3_envs_scale_with_world():
-    p = _run(["--gpus", "3", "--envs", "1000", "--launch-selftest"])
+    p = _run(["--gpus", "3", "--envs", "1000", "--launch-selftest", "--no-cpu-baseline"])
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 3 and d["config"]["global_envs"] == 3000
@@ -50,7 +56,7 @@ def test_external_launcher_world_size_must_match_gpus():
 
 def test_gpus1_runs_in_process():
     # --gpus 1 is the driver's N = 1 command: no launcher, the rank runs here (selftest: gloo world 1)
-    p = _run(["--gpus", "1", "--launch-selftest"],
+    p = _run(["--gpus", "1", "--launch-selftest", "--no-cpu-baseline"],
              env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29611", "WORLD_SIZE": "1", "RANK": "0"})
     assert p.returncode == 0, p.stderr[-3000:]
     assert "launching" not in p.stderr

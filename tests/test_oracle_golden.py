@@ -159,6 +159,26 @@ def test_kernel_blob_matches_fixture():
         d = blob[offs["machu_v"] + np.arange(nu) * 2 * nt + so]
         np.testing.assert_array_equal(d[:-1], (v[1:] - v[:-1]).astype(np.float32))
         assert d[-1] == 0.0
+    # ... and against the fixture: table j's values at the union breakpoints are
+    # the fixture table MACH_1D[j] interpolated there (end-clamped), so a pair / table mix-up that
+    # stays internally consistent (two tables swapped) fails here. The union grid is the header's.
+    mach_1d = ["CDmach", "CYb_M", "Clb_M", "Clda_M", "Cldr_M", "Cma_M", "Cnb_M", "Cnda_M", "Cndr_M"]
+    union = sorted({b for n in mach_1d for b in fns[n]["table"]["rows"]})
+    hdr = re.search(r"BP_machu\[(\d+)\] = \{([^}]*)\}", src)
+    assert int(hdr.group(1)) == nu == len(union)
+    np.testing.assert_array_equal(np.array([float(x.strip().rstrip("f")) for x in hdr.group(2).split(",")], np.float32),
+                                  np.array(union, np.float32))
+    for j, n in enumerate(mach_1d):
+        rows, data = fns[n]["table"]["rows"], fns[n]["table"]["data"]
+        want = np.array([np.interp(x, rows, data) for x in union], np.float64).astype(np.float32)
+        vo, so = _pair_slot(j, nt)
+        got = blob[offs["machu_v"] + np.arange(nu) * 2 * nt + vo]
+        # np.interp clamps at the ends like FGTable; the generator's own fp64 lerp may round the
+        # last bit differently inside a segment, the breakpoints themselves are exact
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-7, err_msg=n)
+        on_bp = np.isin(np.array(union), np.array(rows))
+        np.testing.assert_array_equal(got[on_bp], np.asarray(data, np.float64).astype(np.float32)[
+            np.searchsorted(rows, np.array(union)[on_bp])], err_msg=n)
     v, d = _slopes(m["kCLge"]["data"])
     np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v))], v)
     np.testing.assert_array_equal(blob[offs["kclge_vd"] + 2 * np.arange(len(v)) + 1], d)

@@ -283,6 +283,13 @@ def emit_kernel(model, path):
     offs = {}
 
     def put(key, vals):
+        # every table starts at an even float offset: the kernels read (value, value) /
+        # (slope, slope) and (lo, 1/span) pairs as one 8-byte element (ld2, ds_read_b64), which an
+        # odd-length table before them would silently misalign; the header below
+        # static_asserts it for every OFF_*
+        if len(blob) % 2:
+            blob.append(0.0)
+        assert len(blob) % 2 == 0
         offs[key] = len(blob)
         blob.extend(vals)
 
@@ -429,6 +436,8 @@ def emit_kernel(model, path):
         L.append("#define ENG_NC_%s %d" % (n, nc))
     for k, v in offs.items():
         L.append("#define OFF_%s %d" % (_cname(k), v))
+    for k in offs:
+        L.append('static_assert(OFF_%s %% 2 == 0, "8-byte pair reads need an even float offset");' % _cname(k))
     L.append("")
     L.append("/* breakpoint vectors are also emitted as constexpr arrays so unrolled searches fold")
     L.append(" * them into instruction literals (no LDS reads for breakpoints). */")
