@@ -76,7 +76,10 @@ static int K_ready = 0;
 /* Test-only physics switch (f16ref_set_physics_mask, default 0 = the full model): drops the
  * aerodynamic forces and moments, the thrust, gravity, or J2 (central gravity only), so CPU
  * tests can check the equations of motion against analytic invariants
- * (tests/test_oracle_physics.py). Process-wide; tests set it around their own runs. */
+ * (tests/test_oracle_physics.py); F16REF_TEST_SHAPING_2D is a deliberate defect -- the
+ * PositionReward distance over (x, y) only instead of jsbsim_gym.py:496-500's 3-D norm -- that
+ * the reward parity tests must reject (tests/reward_bound.py). Process-wide; tests set it
+ * around their own runs. */
 static int g_phys_mask = 0;
 void f16ref_set_physics_mask(int mask) { g_phys_mask = mask; }
 static void init_consts(void);
@@ -1009,7 +1012,7 @@ static void env_reset(f16ref* h, int i, const float* goal, const double* ic) {
   for (int k = 0; k < K_; k++) memcpy(e->stack + k * F16_OBS_DIM, f, sizeof f);
   e->head = 0;
   float dx = f[12] - f[0], dy = f[13] - f[1], dz = f[14] - f[2];
-  e->last_d = norm3f(dx, dy, dz);
+  e->last_d = norm3f(dx, dy, (g_phys_mask & F16REF_TEST_SHAPING_2D) ? 0.0f : dz);
 }
 static void write_stack(const f16ref* h, const env_t* e, float* out) {
   const int K_ = h->cfg.stack_k;
@@ -1116,7 +1119,8 @@ int f16ref_step(f16ref* h, const float* act, float* obs, float* rew, uint8_t* te
       tr = e->step >= h->cfg.max_steps; /* env :260 OR gymnasium TimeLimit(1200) */
       /* PositionReward (:493-507) */
       float gx = f[12] - f[0], gy = f[13] - f[1], gz = f[14] - f[2];
-      float dcur = norm3f(gx, gy, gz);
+      /* (F16REF_TEST_SHAPING_2D: the negative control of the reward parity tests) */
+      float dcur = norm3f(gx, gy, (g_phys_mask & F16REF_TEST_SHAPING_2D) ? 0.0f : gz);
       float ddiff = e->last_d - dcur;
       r += h->cfg.goal_gain * (double)ddiff;
       e->last_d = dcur;

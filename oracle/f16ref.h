@@ -57,6 +57,9 @@ int f16ref_n_aero_fns(void);
 #define F16REF_PHYS_NO_THRUST 0x2
 #define F16REF_PHYS_NO_GRAVITY 0x4
 #define F16REF_PHYS_NO_J2 0x8
+/* not physics: a deliberate env-layer defect for negative controls (PositionReward over the
+ * 2-D distance instead of the 3-D one, jsbsim_gym.py:496-500) */
+#define F16REF_TEST_SHAPING_2D 0x10
 void f16ref_set_physics_mask(int mask);
 int f16ref_get_physics_mask(void);
 void f16ref_mass_props(double J[9], double* mass);

@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from parity_tools import frame_err
+from reward_bound import reward_atol
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden", "trajectories.npz")
@@ -60,6 +61,9 @@ def test_gpu_matches_golden_trajectories(gpu, case):
     gold = np.load(GOLD)
     mt = _gen()
     steps, check = (300, mt.CONST_CHECK) if case == "const" else (30, mt.RANDOM_CHECK)
+    # the reward tolerance the frame tolerance in force implies (tests/reward_bound.py): only the
+    # check steps' frames are in the fixture, so the blanket form of the per-lane bound
+    ratol = reward_atol(TOL_CONST300 if case == "const" else TOL_RAND30)
     acts = gold[case + "_act"]
     n = len(gold[case + "_goals"])
     g = F16Envs(n, stack_k=4, seed=3)
@@ -70,7 +74,7 @@ def test_gpu_matches_golden_trajectories(gpu, case):
         out = g.step(ta if acts.ndim == 2 else ta[t - 1].contiguous())
         done = (out.terminated | out.truncated).cpu().numpy().astype(bool)
         np.testing.assert_array_equal(done, gold[case + "_done"][t - 1], err_msg="done @%d" % t)
-        np.testing.assert_allclose(out.rew.cpu().numpy(), gold[case + "_rew"][t - 1], atol=2e-3, err_msg="rew @%d" % t)
+        np.testing.assert_allclose(out.rew.cpu().numpy(), gold[case + "_rew"][t - 1], atol=ratol, err_msg="rew @%d" % t)
         if t in check:
             frames.append(out.obs[:, -1].cpu().numpy())
     g.close()

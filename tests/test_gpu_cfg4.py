@@ -25,6 +25,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs  # noqa: E402
+from reward_bound import reward_atol  # noqa: E402
 from test_gpu_parity import TOL_RAND30, TOL_STEP, _assert_frames  # noqa: E402
 
 from f16_jsb_amd.abi import F16C_EP_COUNT, F16C_STEP  # noqa: E402
@@ -67,7 +68,7 @@ def test_cfg4_rollout_kernel_per_gpu_share(gpu, layout):
         tol = TOL_STEP if t == 0 else TOL_RAND30
         _assert_frames(fr[t], o_prev[:, -1], tol, "slot frame @%d" % t)
         o_r, r_r, te_r, tr_r, *_ = ref.step(a)
-        np.testing.assert_allclose(rw[t], r_r, atol=2e-3, err_msg="reward @%d" % t)
+        np.testing.assert_allclose(rw[t], r_r, atol=reward_atol(TOL_RAND30), err_msg="reward @%d" % t)
         d = (te_r | tr_r).astype(np.float32)
         nxt = st[t + 1] if t + 1 < t30 else last_start
         np.testing.assert_array_equal(nxt, d, err_msg="episode starts @%d" % (t + 1))

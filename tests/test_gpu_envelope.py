@@ -24,6 +24,7 @@ pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs, default_ic  # noqa: E402
 from parity_tools import frame_err  # noqa: E402
+from reward_bound import RewardChecker  # noqa: E402
 from test_gpu_parity import TOL_STEP  # noqa: E402
 
 
@@ -84,15 +85,16 @@ def test_flight_envelope_edges(gpu, cfg5):
     o_r = ref.reset(goals=goals, ic=ic)
     o_g = g.reset(goals=goals, ic=ic).cpu().numpy()
     _assert_frames(o_g[:, -1], o_r[:, -1], TOL_STEP, "IC frame")
+    rc = RewardChecker(o_g, o_r)
     alive = np.ones(n, bool)
     crashes = 0
     for t in range(1, 9):
         a = ref.sample_actions(31, t)
-        o_r, r_r, te_r, tr_r, *_ = ref.step(a)
+        o_r, r_r, te_r, tr_r, tobs_r, *_ = ref.step(a)
         out = g.step(torch.as_tensor(a).cuda())
         te_g = out.terminated.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te_g[alive], te_r[alive], err_msg="terminated @%d" % t)
-        np.testing.assert_allclose(out.rew.cpu().numpy()[alive], r_r[alive], atol=2e-3, err_msg="reward @%d" % t)
+        rc.check(out, o_r, r_r, tobs_r, te_r | tr_r, "reward @%d" % t, mask=alive)
         crashes += int((te_r & alive).sum())
         alive &= ~(te_r | tr_r)
         _assert_frames(out.obs.cpu().numpy()[alive, -1], o_r[alive, -1], TOL_STEP * t, "step %d" % t)

@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs, default_ic  # noqa: E402
 from parity_tools import frame_err  # noqa: E402
+from reward_bound import RewardChecker, assert_rewards_close, final_frames  # noqa: E402
 
 # per frame component atol: lat*R lon*R h mach alpha beta p q r phi theta psi goal(3)
 TOL_STEP = np.array([1e-3, 1e-3, 1e-3, 5e-6, 5e-6, 5e-6, 5e-5, 5e-5, 5e-5, 5e-6, 5e-6, 5e-6, 0, 0, 0])
@@ -122,16 +123,54 @@ def test_random_action_short_horizon(torch_mod):
     rng = np.random.default_rng(3)
     goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
     ref, g = _pair(n, 4, seed=5)
-    ref.reset(goals=goals)
-    g.reset(goals=goals)
+    f_r = ref.reset(goals=goals)[:, -1]
+    f_g = g.reset(goals=goals).cpu().numpy()[:, -1]
+    worst = 0.0
     for t in range(1, 31):
         a = ref.sample_actions(99, t)
-        o_r, r_r, te_r, tr_r, _, _, _ = ref.step(a)
+        o_r, r_r, te_r, tr_r, tobs_r, _, _ = ref.step(a)
         out = g.step(g.sample_actions(99, t))
         np.testing.assert_array_equal(out.terminated.cpu().numpy().astype(bool), te_r)
         np.testing.assert_array_equal(out.truncated.cpu().numpy().astype(bool), tr_r)
-        np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3)
+        o_g = out.obs.cpu().numpy()
+        fin_g, fin_r = final_frames(out, o_g, o_r, tobs_r, te_r | tr_r)
+        worst = max(worst, assert_rewards_close(out.rew.cpu().numpy(), r_r, f_g, f_r, fin_g, fin_r,
+                                                "reward @%d" % t))
+        f_g, f_r = o_g[:, -1], o_r[:, -1]
+    # the derived bound stays at the one-step test's 1e-4 through step 30
+    assert worst <= 1e-4, worst
     _assert_frames(out.obs.cpu().numpy()[:, -1], o_r[:, -1], TOL_RAND30, "random actions @30")
+
+
+def test_reward_bound_rejects_2d_shaping(torch_mod):
+    """Negative control: the oracle with a deliberately 2-D shaping distance
+    (F16REF_TEST_SHAPING_2D: PositionReward over (x, y), jsbsim_gym.py:496-500 without the
+    altitude; the physics untouched) against the HIP path -- the reward check above must reject
+    it within the same 30 steps, on most lane-steps."""
+    from oracle_ref import lib
+    from reward_bound import reward_bound
+    n = 256
+    rng = np.random.default_rng(3)
+    goals = rng.uniform(-5000, 5000, (n, 3)).astype(np.float32)
+    goals[:, 2] = np.abs(goals[:, 2])
+    ref, g = _pair(n, 4, seed=5)
+    L = lib()
+    L.f16ref_set_physics_mask(0x10)
+    try:
+        f_r = ref.reset(goals=goals)[:, -1]
+        f_g = g.reset(goals=goals).cpu().numpy()[:, -1]
+        rejected, moved = 0, 0
+        for t in range(1, 31):
+            o_r, r_r, *_ = ref.step(ref.sample_actions(99, t))
+            out = g.step(g.sample_actions(99, t))
+            o_g, r_g = out.obs.cpu().numpy(), out.rew.cpu().numpy()
+            err = np.abs(r_g.astype(np.float64) - r_r)
+            rejected += int((err > reward_bound(f_g, f_r, o_g[:, -1], o_r[:, -1], r_r)).sum())
+            moved += n
+            f_g, f_r = o_g[:, -1], o_r[:, -1]
+    finally:
+        L.f16ref_set_physics_mask(0)
+    assert rejected >= 0.9 * moved, (rejected, moved)
 
 
 def test_sample_actions_bitexact(torch_mod):
@@ -153,8 +192,7 @@ def test_autoreset_crash_parity(torch_mod):
     ic[:, 7] = -0.6                           # steep dive
     goals = np.tile(np.array([[3000.0, 3000.0, 2000.0]], np.float32), (n, 1))
     ref, g = _pair(n, 4, seed=77)
-    ref.reset(goals=goals, ic=ic)
-    g.reset(goals=goals, ic=ic)
+    rc = RewardChecker(g.reset(goals=goals, ic=ic).cpu().numpy(), ref.reset(goals=goals, ic=ic))
     act = np.zeros((n, 4), np.float32)
     ta = torch.as_tensor(act).cuda()
     saw = np.zeros(n, bool)
@@ -163,10 +201,10 @@ def test_autoreset_crash_parity(torch_mod):
         out = g.step(ta)
         te_g = out.terminated.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te_g, te_r)
+        rc.check(out, o_r, r_r, tobs_r, te_r | tr_r, "reward @%d" % t)  # -10 + shaping on the final frame
         if te_r.any():
             d = te_r
             saw |= d
-            np.testing.assert_allclose(out.rew.cpu().numpy()[d], r_r[d], atol=2e-3)
             np.testing.assert_allclose(out.ep_return.cpu().numpy()[d], eret_r[d], atol=1e-3)
             np.testing.assert_array_equal(out.ep_len.cpu().numpy()[d], elen_r[d])
             _assert_frames(out.terminal_obs.cpu().numpy()[d, -1], tobs_r[d, -1], TOL_CONST300, "terminal obs")
@@ -202,8 +240,7 @@ def test_autoreset_goal_reached_parity(torch_mod):
     goals[48:, 0] = np.linspace(30.0, 600.0, 16)
     goals[48:, 2] = 1524.0 + 400.0                 # out of reach in altitude
     ref, g = _pair(n, 4, seed=91)
-    ref.reset(goals=goals, ic=ic)
-    g.reset(goals=goals, ic=ic)
+    rc = RewardChecker(g.reset(goals=goals, ic=ic).cpu().numpy(), ref.reset(goals=goals, ic=ic))
     act = np.tile(act1, (n, 1))
     ta = torch.as_tensor(act).cuda()
     first = np.zeros(n, bool)
@@ -212,7 +249,7 @@ def test_autoreset_goal_reached_parity(torch_mod):
         out = g.step(ta)
         te_g = out.terminated.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te_g, te_r, err_msg="terminated @%d" % t)
-        np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3, err_msg="reward @%d" % t)
+        rc.check(out, o_r, r_r, tobs_r, te_r | tr_r, "reward @%d" % t)
         d = te_r & ~first  # each env's first episode end (later ones start from a Philox goal)
         if d.any():
             assert (r_r[d] > 9.0).all()  # the +10 goal reward, not the -10 crash

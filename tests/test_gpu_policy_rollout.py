@@ -30,6 +30,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs, default_ic  # noqa: E402
+from reward_bound import reward_atol  # noqa: E402
 from test_gpu_parity import TOL_RAND30, TOL_STEP, _assert_frames, _random_ics  # noqa: E402
 from test_gpu_production import _assert_frames_stat, _stagger  # noqa: E402
 from test_gpu_rollout import numpy_gae  # noqa: E402
@@ -109,7 +110,7 @@ def test_policy_rollout_cfg4_share_vs_oracle(gpu):
         tv, r_raw, te_g, tr_g, tnew = (x.cpu().numpy() for x in vrec[t])
         np.testing.assert_array_equal(te_g.astype(bool), te_r, err_msg="terminated @%d" % t)
         np.testing.assert_array_equal(tr_g.astype(bool), tr_r, err_msg="truncated @%d" % t)
-        np.testing.assert_allclose(r_raw, r_r, atol=2e-3, err_msg="raw reward @%d" % t)
+        np.testing.assert_allclose(r_raw, r_r, atol=reward_atol(TOL_RAND30), err_msg="raw reward @%d" % t)
         # on_policy_algorithm.py:236-245 restated: float32 rewards, gamma * terminal value
         want = r_raw.copy()
         m = tr_r & ~te_r
@@ -322,7 +323,7 @@ def test_persistent_window_rollout_vs_oracle(gpu, k, cfg5):
         else:
             _assert_frames_stat(fr[t], o_prev[:, -1], TOL_RAND30, tol_max, "slot frame @%d" % t)
         o_r, r_r, te_r, tr_r, *_ = ref.step(a)
-        np.testing.assert_allclose(rw[t], r_r, atol=2e-3, err_msg="reward @%d" % t)
+        np.testing.assert_allclose(rw[t], r_r, atol=reward_atol(tol_max), err_msg="reward @%d" % t)
         d = (te_r | tr_r).astype(np.float32)
         nxt = st[t + 1] if t + 1 < T else last
         np.testing.assert_array_equal(nxt, d, err_msg="episode starts @%d" % (t + 1))

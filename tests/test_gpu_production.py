@@ -8,7 +8,8 @@ stack K = 10 (f16_step_gt_kernel, jsbsim_gym.py:58), and BASELINE cfg1 (one env)
 here at its production size against oracle/f16ref.c on identical states and actions:
 
   * done flags, the compacted done list, episode lengths, Philox goal / IC draws: bit-exact;
-  * rewards 2e-3, episode returns 1e-3 (test_gpu_parity.py);
+  * rewards within tests/reward_bound.py's per-lane bound (from the frames' position
+    difference + fp32 rounding; round 6, was a blanket 2e-3), episode returns 1e-3;
   * frames at TOL_RAND30 after 30 random-action steps (test_gpu_parity.py header), reset
     frames at TOL_STEP; cfg5 gust states 1e-4 fps (fp32 Box-Muller vs fp64);
   * a third of the lanes have their step counter staggered (set_state) so that they truncate
@@ -27,6 +28,7 @@ pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs, default_ic  # noqa: E402
 from parity_tools import FRAME_NAMES, frame_err  # noqa: E402
+from reward_bound import assert_rewards_close, final_frames  # noqa: E402
 from test_gpu_parity import TOL_RAND30, TOL_STEP, _assert_frames  # noqa: E402
 
 from f16_jsb_amd.abi import F16C_GUST, F16C_STEP  # noqa: E402
@@ -73,13 +75,20 @@ def _assert_frames_stat(gpu, ref, tol, tol_max, what):
     assert bad.size == 0, "%s: 99.9th percentile of component %d = %.3e > %.1e" % (what, bad[0], p[bad[0]], tol[bad[0]])
 
 
-def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None, early=None, done_list=True):
+def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None, early=None, done_list=True,
+                o_ref0=None):
     """early = (step, tol): every lane's newest frame within tol at that step (before the
     chaotic growth of the fp32-vs-fp64 difference sets in). done_list False: step exactly as
     bench.py does (no caller done list: the windowed handle's bound five-argument launch, and
-    in cfg5 modes the handle's own done list + f16_reset_done_kernel), done flags still checked."""
+    in cfg5 modes the handle's own done list + f16_reset_done_kernel), done flags still checked.
+    Rewards: per lane and step within tests/reward_bound.py's bound, derived from the frames
+    compared (the shaping term moves by at most gain x the position difference, plus fp32
+    rounding). o_ref0: the oracle's observation the run starts from (default: the GPU's, i.e.
+    the caller gave the GPU the oracle's state and observation)."""
     tol_max = tol_final if tol_max is None else tol_max
     n = ref.n
+    f_g_prev = g.obs[:, -1].cpu().numpy()
+    f_r_prev = f_g_prev if o_ref0 is None else np.asarray(o_ref0)[:, -1]
     done_idx = torch.zeros(n, dtype=torch.int32, device=g.device)
     n_done = torch.zeros(1, dtype=torch.int32, device=g.device)
     finished = 0
@@ -94,8 +103,13 @@ def _run_parity(torch, ref, g, steps, seed, tol_final, gust=False, tol_max=None,
         tr_g = out.truncated.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te_g, te_r, err_msg="terminated @%d" % t)
         np.testing.assert_array_equal(tr_g, tr_r, err_msg="truncated @%d" % t)
-        np.testing.assert_allclose(out.rew.cpu().numpy(), r_r, atol=2e-3, err_msg="reward @%d" % t)
+        o_gn = out.obs.cpu().numpy()
+        f_g_now = o_gn[:, -1]
+        # a finished lane's reward is on its final frame, its next last_d on the reset frame
         d = te_r | tr_r
+        fin_g, fin_r = final_frames(out, o_gn, o_r, tobs_r, d)
+        assert_rewards_close(out.rew.cpu().numpy(), r_r, f_g_prev, f_r_prev, fin_g, fin_r, "reward @%d" % t)
+        f_g_prev, f_r_prev = f_g_now, o_r[:, -1]
         if done_list:
             nd = int(n_done.item())
             np.testing.assert_array_equal(np.sort(done_idx[:nd].cpu().numpy()), np.flatnonzero(d),

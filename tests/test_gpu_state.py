@@ -91,7 +91,7 @@ def test_wind_by_reset_ic_switches_kernels(torch_mod):
     o_g = g.reset(goals=goals, ic=ic).cpu().numpy()
     _assert_frames(o_g[:, -1], o_r[:, -1], TOL_STEP, "IC frame")
     assert g.step_kernel_name == "f16_step_var_kernel<2, 1, false>"
-    _run_parity(torch_mod, ref, g, 30, 9, TOL_RAND30)
+    _run_parity(torch_mod, ref, g, 30, 9, TOL_RAND30, o_ref0=o_r)
 
 
 def test_config_wind_selects_wind_kernels(torch_mod):
