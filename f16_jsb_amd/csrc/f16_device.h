@@ -557,14 +557,11 @@ __device__ __forceinline__ f2v ld2(const float* p) {
 __device__ __forceinline__ f2v blend2(float f, f2v v, f2v slope) {
   return __builtin_elementwise_fma(f2v{f, f}, slope, v);
 }
-// Packed fp32 with explicit VOP3P operand modifiers (round 5): one wave alone issues a
-// v_pk_fma_f32 / v_pk_mul_f32 (two fp32 results, each rounded as the scalar instruction rounds it)
-// at the cost of one v_fma_f32 (profiles/r05_floors.json, issue probe), but the compiler turns
-// mixed-sign or swapped operand pairs into v_mov / v_xor shuffles; these spell the half selects
-// (op_sel: the half of each source feeding the low result, op_sel_hi: the high result) and the
-// per-half negations out. MODS is the modifier string, e.g. "op_sel:[1,1] op_sel_hi:[1,0]".
-#define PK_FMA(d, a, b, c, MODS) asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(d) : "v"(a), "v"(b), "v"(c))
-#define PK_MUL(d, a, b, MODS) asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(d) : "v"(a), "v"(b))
+// (No inline asm that emits VALU instructions, round 6: round 5's PK_FMA / PK_MUL macros -- raw
+// v_pk_fma_f32 / v_pk_mul_f32 with hand-written op_sel / neg modifiers -- were opaque to the
+// compiler's scheduler and hazard recognizer; a build that used them inside the 256-register
+// kernels' RunIC faulted. Packed fp32 comes only from the compiler, e.g.
+// blend2's __builtin_elementwise_fma; tests/test_isa_lint.py enforces it.)
 
 // 1-D lookup: literal breakpoints, LDS (lo, 1/span) pairs, LDS (value, slope) pairs
 template <int N>
@@ -1308,12 +1305,11 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
     // n = q (x) p, as the scalar statement
     //   n0 = q0 p0 - q1 p1 - q2 p2 - q3 p3      n1 = q0 p1 + q1 p0 + q2 p3 - q3 p2
     //   n2 = q0 p2 - q1 p3 + q2 p0 + q3 p1      n3 = q0 p3 + q1 p2 - q2 p1 + q3 p0
-    // (fp-contract=on: a product, then three FMAs in that order) in packed pairs (n0, n1),
-    // (n2, n3): per half the same product and FMAs, so the same roundings, in 8 instructions
-    // instead of 16 (the operand halves and signs by VOP3P modifiers, PK_FMA)
-    // (the 256-register two-waves-per-SIMD builds keep the scalar form: the packed operands'
-    // aligned register pairs pushed cfg5's <3, 2> build from 12 to 32 B of scratch)
-    if constexpr (LOWREG) {
+    // (fp-contract=on: a product, then three FMAs in that order). Round 5 issued it as 8 packed
+    // instructions from inline asm in the one-wave builds; round 6 dropped the asm (+10 VALU per
+    // frame): the compiler's own packed form (__builtin_elementwise_fma on the pairs, splats and
+    // swaps left to op_sel folding) put the headline kernel into 40 B of scratch
+    {
       const float q0 = L.q[0], q1 = L.q[1], q2 = L.q[2], q3 = L.q[3];
       const float n0 = q0 * p0 - q1 * p1 - q2 * p2 - q3 * p3;
       const float n1 = q0 * p1 + q1 * p0 + q2 * p3 - q3 * p2;
@@ -1321,21 +1317,6 @@ __device__ __forceinline__ void frame(Lane& L, const float* cmd, double& ce, dou
       const float n3 = q0 * p3 + q1 * p2 - q2 * p1 + q3 * p0;
       const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);  // |n| ~ 1
       L.q[0] = n0 * rn; L.q[1] = n1 * rn; L.q[2] = n2 * rn; L.q[3] = n3 * rn;
-    } else {
-    const f2v Q01 = {L.q[0], L.q[1]}, Q23 = {L.q[2], L.q[3]}, P01 = {p0, p1}, P23 = {p2, p3};
-    f2v m, N01, N23;
-    PK_MUL(m, Q01, P01, "op_sel:[1,1] op_sel_hi:[1,0]");                                 // q1 (p1, p0)
-    PK_FMA(N01, Q01, P01, m, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,1]");         // + q0 (p0, p1)
-    PK_FMA(N01, Q23, P23, N01, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]");       // + q2 (-p2, p3)
-    PK_FMA(N01, Q23, P23, N01, "op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]");  // + q3 (-p3, -p2)
-    PK_MUL(m, Q01, P23, "op_sel:[1,1] op_sel_hi:[1,0]");                                 // q1 (p3, p2)
-    PK_FMA(N23, Q01, P23, m, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,1]");         // + q0 (p2, p3)
-    PK_FMA(N23, Q23, P01, N23, "op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]");       // + q2 (p0, -p1)
-    PK_FMA(N23, Q23, P01, N23, "op_sel:[1,1,0] op_sel_hi:[1,0,1]");                      // + q3 (p1, p0)
-    const float n0 = N01.x, n1 = N01.y, n2 = N23.x, n3 = N23.y;
-    const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);  // |n| ~ 1
-    const f2v R = {rn, rn}, QN01 = N01 * R, QN23 = N23 * R;
-    L.q[0] = QN01.x; L.q[1] = QN01.y; L.q[2] = QN23.x; L.q[3] = QN23.y;
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) L.wI[j] += dt * L.wId[j];

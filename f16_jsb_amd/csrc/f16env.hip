@@ -194,6 +194,10 @@ __device__ __forceinline__ void frame_features_part(const float* o, float* y, in
 // ------------------------------------------------------------------------------------------
 // IC (FGFDMExec::RunIC + InitRunning), mirrors oracle apply_ic()
 // ------------------------------------------------------------------------------------------
+// LOWREG: the enclosing kernel's register budget (frame<LOWREG>: the two-waves-per-SIMD 256-register
+// kernels run their in-kernel RunIC with the same build of the frame as their steps -- round 6;
+// before, every RunIC ran the one-wave build's code, also inside the 256-register kernels)
+template <bool LOWREG = false>
 __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelConsts& C) {
   const double lat = ic[F16_IC_LAT_GEOD_RAD], lon = ic[F16_IC_LON_RAD], h = ic[F16_IC_H_SL_FT];
   // (sincos: one argument reduction per angle, the same values as sin / cos)
@@ -276,7 +280,7 @@ __device__ void apply_ic(Lane& L, const double* ic, const float* T, const ModelC
   // one RunIC per lane from a cold instruction cache, so one copy of the frame code is fetched
   // once and hit twice
 #pragma nounroll
-  for (int pass = 0; pass < 3; ++pass) frame(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
+  for (int pass = 0; pass < 3; ++pass) frame<LOWREG>(L, cmd, ce, se, A, T, C, true F16_STAMP_PASS);
   for (int j = 0; j < 3; ++j) { L.ndv1[j] = -0.0f; L.dv2[j] = 0.0f; L.aIp[j] = L.aI[j]; }  // (dv1 = +0)
 }
 
@@ -450,7 +454,7 @@ __device__ void lane_reset(Lane& L, const SoA& tmpl, const double* ic, const flo
 // lane_reset for a kernel compiled for one MODE (the windowed step's in-step RunIC): the random
 // IC stays a register array (lane_reset selects between it and the global config IC through
 // one pointer, which puts both in scratch)
-template <int MODE>
+template <int MODE, bool LOWREG = false>
 __device__ void lane_reset_mode(Lane& L, const EnvArgs& E, int64_t k, const float* T, const ModelConsts& C,
                                 float* f0) {
   const int32_t ep = L.ep_count;
@@ -465,9 +469,9 @@ __device__ void lane_reset_mode(Lane& L, const EnvArgs& E, int64_t k, const floa
   if (MODE & 1) {
     double ric[F16_IC_N];
     rng_ic(E.seed, gid, (uint32_t)ep, E.ic_lo, E.ic_hi, ric);
-    apply_ic(L, ric, T, C);
+    apply_ic<LOWREG>(L, ric, T, C);
   } else {
-    apply_ic(L, E.ic_cfg, T, C);
+    apply_ic<LOWREG>(L, E.ic_cfg, T, C);
   }
   rng_goal(E.seed, gid, (uint32_t)ep, L.goal);
   L.ep_count = ep + 1;
@@ -922,7 +926,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
           }
           f0[12] = L.goal[0]; f0[13] = L.goal[1]; f0[14] = L.goal[2];
         } else {
-          lane_reset_mode<MODE>(L, a.E, k, sT, a.C, f0);
+          lane_reset_mode<MODE, LOWREG>(L, a.E, k, sT, a.C, f0);
         }
       } else {
 #pragma unroll
@@ -1530,7 +1534,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_rollout_kernel(RollArgs a) {
         fn[12] = L.goal[0]; fn[13] = L.goal[1]; fn[14] = L.goal[2];
         cache_fresh = false;
       } else {
-        lane_reset_mode<MODE>(L, a.E, k, sT, a.C, fn);
+        lane_reset_mode<MODE, OCC == 2>(L, a.E, k, sT, a.C, fn);
         cache_fresh = false;
       }
       last_s = t + 1;

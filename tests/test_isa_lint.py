@@ -102,3 +102,100 @@ def test_fp64_self_differences_are_derive_reference_point(debug):
             bad.append(line.strip())
     assert not bad, "fp64 x - x not narrowed to fp32 (not derive's reference-point difference): %s" % bad[:4]
     assert seen > 0  # the pattern matches the disassembler's syntax (derive's are in there)
+
+
+# ---------------------------------------------------------------------------------------------
+# Round 6: the round-5 memory aperture violation. A build whose derive()
+# formed the body velocity rows and ground speed with raw `asm("v_pk_fma_f32 ...")` (the PK_FMA /
+# PK_MUL macros) faulted in test_persistent_rollout_two_wave_build_matches_fused_steps
+# [contiguous-cfg5] -- f16_rollout_kernel<3, 2>, whose in-kernel RunIC ran that code inside a
+# 256-register kernel with 468 B of spills. Its ISA (rebuilt from commit 81e0cf8 on the CPU, DESIGN.md
+# 8 round 6) passes the three ISA checks below and -verify-machineinstrs, so the faulting access
+# was not located; the mechanism is removed instead: no VALU inline asm in the device sources.
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "f16_jsb_amd", "csrc")
+# asm templates the device code may hold: empty (register pinning / compiler barriers) and the
+# scalar waits / timers it issues explicitly; anything else -- a VALU, VMEM or LDS instruction
+# the compiler cannot see into -- fails
+ASM_ALLOWED = re.compile(r'^(|s_waitcnt [a-z0-9() ]+|s_memtime %0\\n\\ts_waitcnt lgkmcnt\(0\))$')
+
+
+def test_no_valu_inline_asm_in_device_sources():
+    bad, seen = [], 0
+    for fn in sorted(os.listdir(CSRC)):
+        if not fn.endswith((".hip", ".h")):
+            continue
+        src = open(os.path.join(CSRC, fn)).read()
+        for m in re.finditer(r'\basm\s*(?:volatile\s*)?\(\s*"((?:[^"\\]|\\.)*)"', src):
+            seen += 1
+            if not ASM_ALLOWED.match(m.group(1)):
+                line = src.count("\n", 0, m.start()) + 1
+                bad.append("%s:%d: %r" % (fn, line, m.group(1)[:60]))
+        # a macro that pastes an instruction string into asm (round 5's PK_FMA) is the same thing
+        for m in re.finditer(r'#define\s+\w+\([^)]*\)\s+asm\s*\(\s*"([^"]*)"', src):
+            if not ASM_ALLOWED.match(m.group(1)):
+                bad.append("%s: macro asm %r" % (fn, m.group(1)[:60]))
+    assert not bad, "inline asm emitting instructions the compiler cannot schedule or hazard-check: %s" % bad
+    assert seen > 0  # the scan sees the register-pinning asm that is there
+
+
+def _kernels(asm):
+    kernel, body = None, []
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            if kernel:
+                yield kernel, body
+            kernel, body = m.group(1), []
+        elif kernel:
+            body.append(line.strip())
+    if kernel:
+        yield kernel, body
+
+
+def _regs(text):
+    out = set()
+    for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", text):
+        out.update([int(m.group(3))] if m.group(3) else range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="ROCm llvm-objdump not present")
+@pytest.mark.parametrize("debug", BUILDS, ids=["product", "debug"])
+def test_packed_pairs_and_sgpr_spill_lanes(debug):
+    """Two of the round-6 checks of the faulting build, kept on the shipped code objects:
+    (1) every packed fp32 instruction's 64-bit operands are even-aligned register pairs and its
+    destination does not partially overlap a source; (2) a VGPR that holds spilled SGPRs in its
+    lanes (v_writelane / v_readlane) is written by nothing but v_writelane in that kernel."""
+    asm = _disassemble(build_lib(debug))
+    bad, pk = [], 0
+    for kernel, body in _kernels(asm):
+        lanes = set()
+        for ln in body:
+            m = re.match(r"v_(?:writelane|readlane)_b32 (\S+), (\S+),", ln)
+            if m:
+                lanes |= _regs(m.group(1) if ln.startswith("v_writelane") else m.group(2))
+        for ln in body:
+            if ln.startswith("v_pk_") and "f32" in ln:
+                pk += 1
+                ops = [o.strip() for o in ln.split(None, 1)[1].split(",")]
+                pairs = [re.match(r"-?\|?v\[(\d+):(\d+)\]", o) for o in ops]
+                if any(p and int(p.group(1)) % 2 for p in pairs):
+                    bad.append((kernel, "odd pair", ln))
+                d = pairs[0]
+                if d:
+                    dl, dh = int(d.group(1)), int(d.group(2))
+                    for p in pairs[1:]:
+                        if p and (int(p.group(1)), int(p.group(2))) != (dl, dh) and not (
+                                int(p.group(2)) < dl or int(p.group(1)) > dh):
+                            bad.append((kernel, "partial overlap", ln))
+            if lanes and not ln.startswith(("v_writelane", "v_readlane")) and ln.startswith("v_"):
+                first = ln.split(None, 1)[1].split(",")[0] if " " in ln else ""
+                if _regs(first) & lanes:
+                    bad.append((kernel, "spill-lane VGPR written", ln))
+    assert not bad, bad[:6]
+    assert pk > 0  # the packed table blends are in there
+
+
+def build_lib(debug):
+    from f16_jsb_amd.build import build
+    return build(debug=debug)

@@ -46,12 +46,18 @@ def main():
             flags += ["-mllvm", a[len("-mllvm="):]]
     kernel = "_Z22f16_step_win_nt_kernelILi0ELi1ELb0EEvPK15HIP_vector_typeIfLj4EEPKfS3_l8StepArgs"
     dump = None
+    src_asm = None
     args = [a for a in sys.argv[1:] if not a.startswith(("-D", "-f", "-mllvm="))]
     for i, a in enumerate(args):
         if a == "--kernel":
             kernel = args[i + 1]
         if a == "--dump":
             dump = args[i + 1]
+        if a == "--from":  # an existing device-assembly dump (hipcc --cuda-device-only -S): no compile
+            src_asm = args[i + 1]
+    if src_asm:
+        analyse(open(src_asm).read().splitlines(), kernel, flags)
+        return
     with tempfile.TemporaryDirectory() as td:
         out = dump or os.path.join(td, "k.s")
         # the product library's flags (build.py): contraction per source expression, kernarg preload
@@ -61,6 +67,10 @@ def main():
                         "--cuda-device-only", "-S", SRC, "-o", out, *flags], check=True,
                        stderr=subprocess.DEVNULL)
         lines = open(out).read().splitlines()
+    analyse(lines, kernel, flags)
+
+
+def analyse(lines, kernel, flags):
     start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     body = lines[start:end]
