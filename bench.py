@@ -499,6 +499,7 @@ def rollout_bench(args, dev, rank, world):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     shard_bytes = sum(v.numel() * v.element_size() for v in buf.state_dict().values())
+    step_kernel = envs.step_kernel_name  # (before close: the name is the handle's)
     envs.close()
     del buf
     torch.cuda.empty_cache()
@@ -517,7 +518,7 @@ def rollout_bench(args, dev, rank, world):
         "fused_over_plain_step": round(fused_ms / plain_ms, 4),
         "rollout_step_kernel_ms": round(roll_kern_ms, 5),
         "window_step_kernel_ms_same_envs": round(step_kern_ms, 5),
-        "rollout_step_kernel": envs.step_kernel_name.replace("false>", "true>") + " (the rollout-slot build)",
+        "rollout_step_kernel": step_kernel.replace("false>", "true>") + " (the rollout-slot build)",
         **cont,
         "gae_ms": round(float(tt[1]) * 1e3, 3),
         "gae_kernel_ms": round(float(tt[4]), 4),
@@ -747,6 +748,39 @@ def telemetry_bench(envs, stream, iters=200):
             "timing": "HIP-graph replay of %d launches (kernel + launch boundary)" % iters if gms is not None
             else "host-driven launches", "host_driven_ms": round(host_ms, 5),
             "achieved_GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_env": 100}
+
+
+def sampler_bench(envs, stream, batches=64, iters=20):
+    """The action sampler beside the headline (jsbsim_gym.py:575's action_space.sample() per env,
+    the device Philox stream): `batches` steps' actions for every env in ONE launch
+    (f16env_sample_actions_steps), 16 B per env-step written; and the one-batch launch
+    (f16env_sample_actions) under graph replay for comparison (launch-latency-bound: 1 MB per
+    launch at 65 536 envs). Kernel time from HIP events on the launch stream."""
+    import torch
+    n = envs.n
+    out = envs.sample_actions(7, 0, steps=batches)
+    for _ in range(3):
+        envs.sample_actions(7, 0, out=out, steps=batches)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for i in range(iters):
+        envs.sample_actions(7, i * batches, out=out, steps=batches)
+    e.record(stream)
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    nbytes = batches * n * 16
+    one = torch.empty((n, 4), dtype=torch.float32, device=envs.device)
+    g1 = graph_ms(lambda: envs.sample_actions(7, 0, out=one), 200)
+    gbps = nbytes / (ms * 1e-3) / 1e9
+    del out
+    return {"kernel": "f16_sample_actions_steps_kernel", "envs": n, "batches_per_launch": batches,
+            "ms_per_launch": round(ms, 5), "bytes_per_launch": nbytes, "achieved_GBps": round(gbps, 1),
+            "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBPS, 4),
+            "env_steps_per_s": round(batches * n / (ms * 1e-3), 1),
+            "one_batch_launch_ms_graph": None if g1 is None else round(g1, 5),
+            "one_batch_frac_of_hbm_peak": None if g1 is None else round(n * 16 / (g1 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "timing": "HIP events around %d back-to-back launches (multi-step); graph replay of 200 launches "
+                      "(one batch)" % iters}
 
 
 def persistent_bench(dev, n, stack, steps, seed):
@@ -993,12 +1027,12 @@ def main():
     venv.reset()
     burn = spread_phases(envs, args, dev)
     pool = args.action_pool if args.action_pool > 0 else args.steps
-    acts = torch.empty((pool, n, 4), dtype=torch.float32, device=dev)
-    for t in range(pool):
-        envs.sample_actions(args.seed + 1000, t, out=acts[t])
+    # the run's actions pre-generated in HBM by ONE launch each (f16env_sample_actions_steps: the
+    # same draws as one f16env_sample_actions launch per step)
+    acts = envs.sample_actions(args.seed + 1000, 0, steps=pool)
     warm = torch.empty((max(args.warmup, 1), n, 4), dtype=torch.float32, device=dev)
-    for t in range(args.warmup):
-        envs.sample_actions(args.seed + 2000, t, out=warm[t])
+    if args.warmup > 0:
+        envs.sample_actions(args.seed + 2000, 0, out=warm[:args.warmup], steps=args.warmup)
     from f16_jsb_amd.abi import F16C_EP_COUNT
     stream = torch.cuda.current_stream(dev)
     start_ev, end_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1064,6 +1098,7 @@ def main():
 
     feat = leg("features", features_bench, envs, stream)
     telem = leg("telemetry", telemetry_bench, envs, stream)
+    sampler = leg("sampler", sampler_bench, envs, stream)
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, gpu_ms_per_step, kern_min_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -1180,6 +1215,7 @@ def main():
         },
         "features": feat,
         "telemetry": telem,
+        "sampler": sampler,
     }
     if rollout is not None:
         out["rollout"] = rollout

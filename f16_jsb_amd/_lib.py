@@ -76,6 +76,8 @@ def lib():
     _set(L, "f16env_window_step_ex", [vp, vp, vp, i32, i32, ctypes.c_uint32, u64, u64], i32)
     _set(L, "f16env_window_step_ex_kernel_name", [vp, ctypes.c_uint32], ctypes.c_char_p)
     _set(L, "f16env_window_poses_bind", [vp, vp], i32)
+    _set(L, "f16env_window_resets_deferred", [vp], i32)
+    _set(L, "f16env_sample_actions_steps", [vp, vp, u64, u64, i32, vp], i32)
     _set(L, "f16env_bootstrap_timeouts", [vp, i64, vp, vp, vp, vp, ctypes.c_double], i32)
     _set(L, "f16env_bootstrap_stash", [vp, i64, i32, vp, i64, i64, vp, vp, i64, vp, vp, vp, i64], i32)
     _set(L, "f16env_bootstrap_apply", [vp, i64, vp, vp, vp, ctypes.c_double], i32)
@@ -128,6 +130,7 @@ EXPORTED_SYMBOLS = (
     "f16env_step_mode", "f16env_features_strided", "f16env_features_window_step", "f16env_set_window_order", "f16env_window_clear_fresh",
     "f16env_window_bind", "f16env_window_step_bound", "f16env_window_feature_bind", "f16env_step_window_nt", "f16env_window_step_rollout",
     "f16env_window_step_ex", "f16env_window_step_ex_kernel_name", "f16env_window_poses_bind",
+    "f16env_window_resets_deferred", "f16env_sample_actions_steps",
     "f16env_window_rollout_random", "f16env_bootstrap_timeouts", "f16env_bootstrap_stash", "f16env_bootstrap_apply", "f16env_abi_version",
     "f16env_get_state",
     "f16env_set_state", "f16env_trim", "f16env_sample_actions", "f16env_gae", "f16env_features", "f16env_poses", "f16env_step_kernel_name", "f16env_step_waves_per_simd", "f16env_step_variant", "f16env_profile_begin", "f16env_profile_end", "f16env_profile_times",

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 
-F16ENV_ABI_VERSION = 5  # include/f16env.h (checked against f16env_abi_version() at load)
+F16ENV_ABI_VERSION = 6  # include/f16env.h (checked against f16env_abi_version() at load)
 F16_OBS_DIM = 15
 F16_ACT_DIM = 4
 

@@ -31,8 +31,10 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = False, o1: bool = False) -> str:
-    out = OUT_DEBUG if debug else (OUT_O1 if o1 else OUT)
+def build(verbose: bool = False, force: bool = False, extra=(), debug: bool = False, o1: bool = False,
+          out: str | None = None) -> str:
+    """out: another library path (A/B variants, tools/ab_builds.py); default the product's."""
+    out = out or (OUT_DEBUG if debug else (OUT_O1 if o1 else OUT))
     if debug:
         extra = tuple(extra) + ("-DF16_DEBUG_CHECKS",)
     if o1:

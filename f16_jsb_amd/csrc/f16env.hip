@@ -999,7 +999,43 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
     // store instruction writes 1 KiB contiguous (16 whole slots, 4 lanes per slot) instead of a
     // 16-B quarter of every slot. Swizzle: quarter j of slot r at float4 r*4 + (j ^ (r>>2 & 3)),
     // conflict-free on both the per-lane writes and the per-slot reads.
-    if (rows == EPW) {
+    // A wave none of whose lanes was reset now (~94 % of waves in the bench's steady state) has
+    // the same 64 slots for both histories: one LDS staging pass, each transposed float4 read
+    // once and stored twice (round 6; was two passes for every wave: 4 ds_write_b128 + 4
+    // ds_read_b128 and two wave barriers per wave per step saved). The byte count is unchanged:
+    // both histories must hold every frame for the (N, K, 15) strided view to alternate parity
+    // (DESIGN.md 9 item 7).
+#ifdef F16_TWO_PASS_SLOTS  // (A/B reference: round 5's two staging passes for every wave)
+    const bool one_pass = false;
+#else
+    const bool one_pass = !ROLL && rows == EPW && __ballot(reset_now) == 0;
+#endif
+    if (one_pass) {
+      float4* st4 = reinterpret_cast<float4*>(stg);
+      const int q = lane & 3, sw = (lane >> 2) & 3;
+      __builtin_amdgcn_wave_barrier();
+      st4[lane * 4 + (0 ^ sw)] = make_float4(f[0], f[1], f[2], f[3]);
+      st4[lane * 4 + (1 ^ sw)] = make_float4(f[4], f[5], f[6], f[7]);
+      st4[lane * 4 + (2 ^ sw)] = make_float4(f[8], f[9], f[10], f[11]);
+      st4[lane * 4 + (3 ^ sw)] = make_float4(f[12], f[13], f[14], 0.0f);
+      __builtin_amdgcn_wave_barrier();
+      const int64_t off = (int64_t)p * a.wrow + (row0 + (lane >> 2)) * a.wenv + 4 * q;
+      float* const dx = a.wx + off;
+      float* const dy = a.wy + off;
+      float4 v[EPW / 16];
+#pragma unroll
+      for (int j = 0; j < EPW / 16; ++j) {
+        const int r = 16 * j + (lane >> 2);
+        v[j] = st4[r * 4 + (q ^ ((r >> 2) & 3))];
+      }
+#pragma unroll
+      for (int j = 0; j < EPW / 16; ++j) st16<NT>(reinterpret_cast<float4*>(dx + (int64_t)(16 * j) * a.wenv), v[j]);
+#ifndef F16_DIAG_ONE_HIST  // (timing-only bound of a single history: wrong results by design, never shipped)
+#pragma unroll
+      for (int j = 0; j < EPW / 16; ++j) st16<NT>(reinterpret_cast<float4*>(dy + (int64_t)(16 * j) * a.wenv), v[j]);
+#endif
+      __builtin_amdgcn_wave_barrier();
+    } else if (rows == EPW) {
       float4* st4 = reinterpret_cast<float4*>(stg);
       const int q = lane & 3, sw = (lane >> 2) & 3;
       float* const hist[2] = {a.wx, a.wy};
@@ -1907,6 +1943,24 @@ __global__ void f16_sample_actions_kernel(int64_t n, int64_t id_base, uint64_t s
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   reinterpret_cast<float4*>(act)[k] = philox_action(seed, (uint64_t)(id_base + k), step);
+}
+// T steps' actions in one launch (f16env_sample_actions_steps, ABI 6): act[t][k] for t < T, the
+// same draws as T calls of f16env_sample_actions. One 1-MB batch per launch (65 536 envs) is a
+// launch-latency-bound kernel (~0.8 us over an empty launch, at 1 wave per SIMD); here each lane
+// draws SA_PER_LANE float4 at a grid stride, so the whole T x N block fills the chip and streams
+// out as coalesced 1-KiB wave stores.
+constexpr int SA_PER_LANE = 4;
+__global__ __launch_bounds__(BLOCK) void f16_sample_actions_steps_kernel(int64_t n, int64_t total, int64_t id_base,
+                                                                        uint64_t seed, uint64_t step0, float* act) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < SA_PER_LANE; ++u, i += stride) {
+    if (i < total) {
+      const int64_t t = i / n, k = i - t * n;
+      st16<true>(reinterpret_cast<float4*>(act) + i, philox_action(seed, (uint64_t)(id_base + k), step0 + (uint64_t)t));
+    }
+  }
 }
 
 // GAE(lambda) over a [n_steps][n_envs] rollout, one lane per env, backward in time.
@@ -3183,6 +3237,27 @@ int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step
                      (int64_t)h->soa.n, (int64_t)h->cfg.env_id_base, seed, step, act);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+int f16env_sample_actions_steps(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T, float* act) {
+  if (!h || !act) return set_err(-1, "null argument");
+  if (T <= 0) return set_err(-1, "T must be > 0");
+  if (((uintptr_t)act & 15) != 0) return set_err(-1, "act must be 16-byte aligned");
+  const int64_t total = (int64_t)T * h->soa.n;
+  const int64_t per_block = (int64_t)BLOCK * SA_PER_LANE;
+  const int64_t blocks = (total + per_block - 1) / per_block;
+  if (blocks > 0x7fffffff) return set_err(-1, "T x N too large");
+  hipLaunchKernelGGL(f16_sample_actions_steps_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, (hipStream_t)stream,
+                     (int64_t)h->soa.n, total, (int64_t)h->cfg.env_id_base, seed, step0, act);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int f16env_window_resets_deferred(f16env_t h) {
+  if (!h) return set_err(-1, "null handle");
+  // cfg5 modes with F16ENV_ICC_PERIOD=0: finished lanes are reset by f16_reset_done_kernel after
+  // the step kernel (the same condition f16env_step_window tests: `deferred`)
+  return (h->mode && !(h->cfg.flags & F16_FLAG_NO_AUTORESET) && h->icc_period <= 0) ? 1 : 0;
 }
 
 int f16env_gae(void* stream, int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,

@@ -160,6 +160,13 @@ class F16Envs:
             self._step_bound = L.f16env_window_step_bound
             self._step_ex = L.f16env_window_step_ex
             self.terminal_obs = self._window(1)
+            if (self.fused_features or self.fused_poses) and L.f16env_window_resets_deferred(h):
+                # the deferred-reset step (cfg5 with F16ENV_ICC_PERIOD=0): the epilogue extras
+                # would describe the pre-reset window, and f16env_window_step_ex refuses them --
+                # refused here instead of at the first step
+                self.close()
+                raise ValueError("fused_features / fused_poses are not available with the deferred-reset "
+                                 "windowed step (cfg5 with F16ENV_ICC_PERIOD=0)")
             if self.fused_features:
                 self._feature_hist()
             if self.fused_poses:
@@ -673,11 +680,28 @@ class F16Envs:
         check(lib().f16env_trim(self._h, self._stream(), _ptr(c), _ptr(out), _ptr(res)), "f16env_trim")
         return out, res
 
-    def sample_actions(self, seed: int, step: int, out=None):
+    def sample_actions(self, seed: int, step: int, out=None, steps: int | None = None):
+        """Uniform Box actions from the device Philox stream keyed by (seed, env id, step)
+        (action_space.sample() per env, jsbsim_gym.py:143-148): (N, 4) for `step`, or with
+        `steps` = T the (T, N, 4) batches of steps step .. step+T-1 in ONE launch
+        (f16env_sample_actions_steps, bit-identical to T single calls)."""
+        t = self.torch
+        if steps is None:
+            if out is None:
+                out = t.empty((self.n, 4), dtype=t.float32, device=self.device)
+            if tuple(out.shape) != (self.n, 4) or not out.is_contiguous():
+                raise ValueError("out must be a contiguous (N, 4) float32 tensor")
+            check(lib().f16env_sample_actions(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                              int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(out)), "f16env_sample_actions")
+            return out
+        T = int(steps)
         if out is None:
-            out = self.torch.empty((self.n, 4), dtype=self.torch.float32, device=self.device)
-        check(lib().f16env_sample_actions(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                                          int(step) & 0xFFFFFFFFFFFFFFFF, _ptr(out)), "f16env_sample_actions")
+            out = t.empty((T, self.n, 4), dtype=t.float32, device=self.device)
+        if tuple(out.shape) != (T, self.n, 4) or not out.is_contiguous():
+            raise ValueError("out must be a contiguous (steps, N, 4) float32 tensor")
+        check(lib().f16env_sample_actions_steps(self._h, self._stream(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                int(step) & 0xFFFFFFFFFFFFFFFF, T, _ptr(out)),
+              "f16env_sample_actions_steps")
         return out
 
 

@@ -52,8 +52,10 @@ extern "C" {
  * (+ F16_SLOT_FEATURE_WINDOW), f16env_abi_version.
  * 4 (round 5): new f16env_window_step_ex (in-step action draws, F16_STEP_FEATURE_WINDOW) and
  * f16env_window_step_ex_kernel_name; nothing else changed.
- * 5 (round 5): new F16_STEP_POSES flag and f16env_window_poses_bind; nothing else changed. */
-#define F16ENV_ABI_VERSION 5
+ * 5 (round 5): new F16_STEP_POSES flag and f16env_window_poses_bind; nothing else changed.
+ * 6 (round 6): new f16env_sample_actions_steps and f16env_window_resets_deferred; nothing else
+ * changed. */
+#define F16ENV_ABI_VERSION 6
 
 /* Frame layout (jsbsim_gym.py:12-25 STATE_FORMAT + goal, :172-197) */
 #define F16_OBS_DIM 15
@@ -303,6 +305,14 @@ int f16env_window_clear_fresh(f16env_t h, void* stream);
  * is the non-temporal-store build (1: the whole grid resident in one round of waves). */
 int f16env_step_window_waves_per_simd(f16env_t h);
 int f16env_step_window_nt(f16env_t h);
+/* ABI 6. 1 when this handle's windowed step leaves its finished lanes to the deferred reset
+ * kernel that runs after it (cfg5 modes with F16ENV_ICC_PERIOD=0), 0 when the step resets them
+ * itself (the reference task's template reset, cfg5's reset cache) or nobody does
+ * (F16_FLAG_NO_AUTORESET). The epilogue extras of f16env_window_step_ex (F16_STEP_POSES,
+ * F16_STEP_FEATURE_WINDOW) and the rollout slot's next_frame / features are refused while it
+ * reads 1 (they would describe the pre-reset window); the Python front end refuses fused_poses /
+ * fused_features handles at construction by it. <0 on a NULL handle. */
+int f16env_window_resets_deferred(f16env_t h);
 
 /* One env step that also fills one slot of a device rollout buffer (SURVEY.md 8f rank 1,
  * replacing the per-step stable_baselines3 RolloutBuffer.add, buffers.py:440-479, and the
@@ -438,6 +448,10 @@ int f16env_trim(f16env_t h, void* stream, const double* ic_in, double* ic_out,
 /* Uniform actions over the Box [-1,-1,-1,0]..[1,1,1,1] from Philox4x32-10 keyed by
  * (seed; global env id, step). act: N x 4 float. */
 int f16env_sample_actions(f16env_t h, void* stream, uint64_t seed, uint64_t step, float* act);
+/* ABI 6. T batches in one launch: act = T x N x 4 float (16-B aligned), act[t] the batch
+ * f16env_sample_actions(seed, step0 + t) draws, bit for bit (a caller pre-generating a run's
+ * actions -- bench.py -- makes one launch instead of T). */
+int f16env_sample_actions_steps(f16env_t h, void* stream, uint64_t seed, uint64_t step0, int32_t T, float* act);
 
 /* GAE(lambda) advantages and returns over a device rollout laid out [n_steps][n_envs]
  * (float32; episode_starts as 0/1 float, dones uint8 for the step after the last), restating

@@ -105,6 +105,9 @@ def test_null_handle_calls_return_errors(so_path):
     assert L.f16env_profile_times(None, None, 4) < 0
     assert L.f16env_window_restart(None, None, None, None, 8, 7) < 0
     assert L.f16env_reset_window(None, None, None, None, None, None, 8, 3) < 0
+    # ABI 6
+    assert L.f16env_window_resets_deferred(None) < 0
+    assert L.f16env_sample_actions_steps(None, None, 1, 0, 4, None) < 0
     # features on a strided block: bad shapes / strides are refused before any launch
     assert L.f16env_features_strided(None, 4, 0, None, 16, 16, None) < 0
     assert L.f16env_features_strided(None, 4, 2, None, -1, 16, None) < 0
