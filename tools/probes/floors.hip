@@ -43,7 +43,9 @@ __global__ __launch_bounds__(BLOCK, 1) void k_empty_lds(float* out) {
 }
 
 // the step's byte pattern, LPE lanes per env
-template <int LPE, bool NT>
+// BLK (round 6): the state wave-blocked -- env k's column j at (k / 64) * 64 * NCOL + j * 64 + k % 64,
+// so a wave's 16 columns are one contiguous 16 KiB block instead of 16 1-KiB pieces n * 16 B apart
+template <int LPE, bool NT, bool BLK = false>
 __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, const float4* __restrict__ act, int64_t n,
                                                    float* __restrict__ h0, float* __restrict__ h1, int32_t pos,
                                                    float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
   constexpr int CPL = NCOL / LPE;  // columns per lane
   float4 c[CPL];
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) c[j] = sc[(int64_t)(sub + LPE * j) * n + k];
+  for (int j = 0; j < CPL; ++j)
+    c[j] = BLK ? sc[(k >> 6) * (64 * NCOL) + j * 64 + (k & 63)] : sc[(int64_t)(sub + LPE * j) * n + k];
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (sub == 0) a = act[k];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
   typedef float v4f __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    float4* p = sc + (int64_t)(sub + LPE * j) * n + k;
+    float4* p = BLK ? sc + (k >> 6) * (64 * NCOL) + j * 64 + (k & 63) : sc + (int64_t)(sub + LPE * j) * n + k;
     const float4 v = make_float4(c[j].x + 1.0f, c[j].y, c[j].z, c[j].w);
     if (NT) __builtin_nontemporal_store(__builtin_bit_cast(v4f, v), reinterpret_cast<v4f*>(p));
     else *p = v;
@@ -320,6 +323,9 @@ int main(int argc, char** argv) {
   copy_line("copy_nt_4wave", 4, k_copy<4, true>);
   copy_line("copy_plain_1wave", 1, k_copy<1, false>);
   copy_line("copy_plain_4wave", 4, k_copy<4, false>);
+  copy_line("copy_nt_1wave_blocked", 1, k_copy<1, true, true>);
+  copy_line("copy_plain_1wave_blocked", 1, k_copy<1, false, true>);
+  copy_line("copy_nt_1wave_again", 1, k_copy<1, true>);
   const int iters = 256;
   for (int blocks : {256}) {
     issue_probe<F_FMA>(out, cyc, blocks, iters);
