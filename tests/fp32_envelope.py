@@ -41,8 +41,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from f16_jsb_amd.abi import (F16C_AI, F16C_AIP, F16C_BA, F16C_LX, F16C_Q,  # noqa: E402
-                             F16C_TEF, F16C_VI, F16C_VIH1, F16C_VIH2, F16C_WI, F16C_WID, F16L_N)
+from f16_jsb_amd.abi import (F16C_AI, F16C_AIP, F16C_BA, F16C_GUST, F16C_LX, F16C_Q,  # noqa: E402
+                             F16C_TEF, F16C_VI, F16C_VIH1, F16C_VIH2, F16C_WI, F16C_WID, F16C_WIND, F16L_N)
 from parity_tools import FRAME_NAMES, frame_err  # noqa: E402
 
 HORIZONS = (1, 3, 10, 30, 100, 300, 1199)
@@ -50,7 +50,8 @@ VARIANTS = ("control", "round1", "ulp1", "round")
 # fields the HIP kernel holds in fp32: attitude, rates and their derivatives, the
 # AB2 acceleration history, FCS actuators + PID states, engine, the auxiliary latch
 F32_FIELDS = np.r_[F16C_AI:F16C_AI + 3, F16C_AIP:F16C_AIP + 3, F16C_Q:F16C_Q + 4, F16C_WI:F16C_WI + 3,
-                   F16C_WID:F16C_WID + 3, F16C_BA:F16C_BA + 3, F16C_TEF:F16C_LX + F16L_N]
+                   F16C_WID:F16C_WID + 3, F16C_BA:F16C_BA + 3, F16C_TEF:F16C_LX + F16L_N,
+                   F16C_WIND:F16C_GUST + 3]  # (cfg5: steady wind and gust, fp32 columns of the wind kernels)
 
 
 def workload(n):
@@ -83,20 +84,21 @@ def one_ulp(s, rng):
     return s
 
 
-def run(n=256, steps=1199, horizons=HORIZONS, variants=VARIANTS, seed=5, act_seed=99, hip=False):
-    """{variant: {horizon: {"lanes": m, component: [p50, p99, max]}}} -- see the module doc."""
+def run(n=256, steps=1199, horizons=HORIZONS, variants=VARIANTS, seed=5, act_seed=99, hip=False, cfg5=False):
+    """{variant: {horizon: {"lanes": m, component: [p50, p99, max]}}} -- see the module doc.
+    cfg5: BASELINE cfg5's randomised ICs + Gauss-Markov gusts (the same goals)."""
     from oracle_ref import OracleEnvs
     goals = workload(n)
-    envs = {"ref": OracleEnvs(n, stack_k=4, seed=seed)}
+    envs = {"ref": OracleEnvs(n, stack_k=4, seed=seed, cfg5=cfg5)}
     for v in variants:
-        envs[v] = OracleEnvs(n, stack_k=4, seed=seed)
+        envs[v] = OracleEnvs(n, stack_k=4, seed=seed, cfg5=cfg5)
     for e in envs.values():
         e.reset(goals=goals)
     g = None
     if hip:
         import torch
         from f16_jsb_amd.env import F16Envs
-        g = F16Envs(n, stack_k=4, seed=seed, obs_layout="window")
+        g = F16Envs(n, stack_k=4, seed=seed, obs_layout="window", cfg5=cfg5)
         g.reset(goals=torch.as_tensor(goals))
         variants = tuple(variants) + ("hip",)
     rng = np.random.default_rng(1234)
@@ -142,8 +144,9 @@ def main():
     ap.add_argument("--steps", type=int, default=1199)
     ap.add_argument("--json", default=None)
     ap.add_argument("--gpu", action="store_true", help="also the HIP path on cuda:0 (the GPU box)")
+    ap.add_argument("--cfg5", action="store_true", help="BASELINE cfg5: random ICs + gusts")
     args = ap.parse_args()
-    out = run(args.n, args.steps, hip=args.gpu)
+    out = run(args.n, args.steps, hip=args.gpu, cfg5=args.cfg5)
     for v, per in out.items():
         for t, d in per.items():
             print("%-7s t=%-5d lanes=%-4d h_m p99 %.3e max %.3e | alpha p99 %.3e | phi p99 %.3e | lat*R p99 %.3e"

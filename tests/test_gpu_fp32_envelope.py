@@ -34,8 +34,12 @@ HORIZONS = (1, 10, 30, 100, 300, 1199)
 FACTOR = 3.0
 
 
-def test_hip_divergence_within_fp32_envelope(gpu):
-    out = run(n=256, steps=1199, horizons=HORIZONS, variants=("ulp1", "round"), hip=True)
+@pytest.mark.parametrize("cfg5", [False, True], ids=["reference_task", "cfg5"])
+def test_hip_divergence_within_fp32_envelope(gpu, cfg5):
+    """cfg5: BASELINE cfg5's random ICs (up to 1 200 fps, 3 000-30 000 ft) and Gauss-Markov gusts
+    on the same lanes; the envelope's `round` variant then also rounds the steady-wind and gust
+    states (fp32 columns of the wind kernels)."""
+    out = run(n=256, steps=1199, horizons=HORIZONS, variants=("ulp1", "round"), hip=True, cfg5=cfg5)
     table = {}
     worst = {}
     for t in HORIZONS:
@@ -51,6 +55,8 @@ def test_hip_divergence_within_fp32_envelope(gpu):
             worst[(t, nm)] = (hip, bound)
         table[t] = row
     path = os.environ.get("F16_ENVELOPE_JSON")
+    if path and cfg5:
+        path = path.replace(".json", "_cfg5.json")
     if path:
         with open(path, "w") as f:
             json.dump({"test": "tests/test_gpu_fp32_envelope.py", "factor": FACTOR,
