@@ -1052,11 +1052,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # the per-step action views made before the clock starts (indexing acts[t] in the loop costs
+    # the host ~2 us per step -- on the critical path of the first launch of a short region)
+    act_views = acts.unbind(0)
     gc.disable()  # no collector pause inside the timed steps (a gc.collect() here idles the GPU ~50 ms)
     t0 = time.perf_counter()
     start_ev.record(stream)
     for t in range(args.steps):
-        envs.step(acts[t % pool])
+        envs.step(act_views[t % pool])
     end_ev.record(stream)
     torch.cuda.synchronize()
     # each rank's own K steps, barrier to barrier; the job's time is the max over ranks (all_reduce
