@@ -45,12 +45,26 @@ __global__ __launch_bounds__(BLOCK, 1) void k_empty_lds(float* out) {
 // the step's byte pattern, LPE lanes per env
 // BLK (round 6): the state wave-blocked -- env k's column j at (k / 64) * 64 * NCOL + j * 64 + k % 64,
 // so a wave's 16 columns are one contiguous 16 KiB block instead of 16 1-KiB pieces n * 16 B apart
-template <int LPE, bool NT, bool BLK = false>
+// STG (round 6): also the step's table staging -- a 12.3 KB blob per workgroup by LDS-DMA, issued
+// before the state loads and retired by the same wait, as f16_step_win_nt_kernel does
+constexpr int BLOB_FLOATS = 3080;
+__device__ __attribute__((aligned(16))) float g_blob[BLOB_FLOATS];
+template <int LPE, bool NT, bool BLK = false, bool STG = false>
 __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, const float4* __restrict__ act, int64_t n,
                                                    float* __restrict__ h0, float* __restrict__ h1, int32_t pos,
                                                    float* __restrict__ rew, uint8_t* __restrict__ term,
                                                    uint8_t* __restrict__ trunc) {
   __shared__ __align__(16) float4 stg[4][64 * 4];
+  __shared__ __align__(16) float sT[STG ? BLOB_FLOATS : 4];
+  if (STG) {
+    const int wave_base = threadIdx.x & ~63;
+    for (int r = 0; r < BLOB_FLOATS / 4; r += BLOCK) {
+      const int piece = r + threadIdx.x;
+      if (piece < BLOB_FLOATS / 4)
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g_blob + 4 * piece),
+                                         (void __attribute__((address_space(3)))*)(sT + 4 * (r + wave_base)), 16, 0, 0);
+    }
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const int64_t k = t / LPE;
@@ -64,9 +78,11 @@ __global__ __launch_bounds__(BLOCK, 1) void k_copy(float4* __restrict__ sc, cons
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (sub == 0) a = act[k];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (STG) __syncthreads();
   // a trivially dependent "frame": 16 floats from what was loaded
   float4 f[4];
   f[0] = make_float4(c[0].x + a.x, c[0].y + a.y, c[0].z + a.z, c[0].w + a.w);
+  if (STG) f[0].x += sT[(threadIdx.x * 7) % BLOB_FLOATS];
 #pragma unroll
   for (int j = 1; j < 4; ++j) f[j] = c[j % CPL];
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -326,6 +342,8 @@ int main(int argc, char** argv) {
   copy_line("copy_nt_1wave_blocked", 1, k_copy<1, true, true>);
   copy_line("copy_plain_1wave_blocked", 1, k_copy<1, false, true>);
   copy_line("copy_nt_1wave_again", 1, k_copy<1, true>);
+  copy_line("copy_nt_1wave_staged", 1, k_copy<1, true, false, true>);
+  copy_line("copy_nt_1wave_again2", 1, k_copy<1, true>);
   const int iters = 256;
   for (int blocks : {256}) {
     issue_probe<F_FMA>(out, cyc, blocks, iters);
