@@ -11,12 +11,14 @@ Each case runs three handles on identical inputs for 15 steps:
     build.py -ffp-contract=on); and the windowed handle's feature window (obs_features) equal
     to the whole-window feature transform;
   * the contiguous layout against the CPU oracle (oracle/f16ref.c): done flags and episode lengths
-    bit-exact, rewards 2e-3, newest frames within the random-action tolerance of
+    bit-exact, rewards within the frame-derived bound (tests/reward_bound.py), newest frames within the random-action tolerance of
     tests/test_gpu_parity.py (the cfg5 transonic tail statistically, as test_gpu_production.py);
   * the diagnostic counters (quarantines, out-of-bounds frames) equal on the two GPU layouts
     and, for the out-of-bounds count, equal to the oracle's.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import pytest
@@ -24,6 +26,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 from oracle_ref import OracleEnvs  # noqa: E402
+from reward_bound import reward_atol  # noqa: E402
 from test_gpu_parity import TOL_RAND30, _assert_frames, _random_ics  # noqa: E402
 from test_gpu_production import _assert_frames_stat  # noqa: E402
 
@@ -51,7 +54,9 @@ def _cases(n_cases=64, seed=2026):
     return out
 
 
-CASES = _cases()
+# F16_FUZZ_CASES: more cases for a one-off robustness run (the suite draws 64; the same seed, so the
+# first 64 of a longer run are the suite's)
+CASES = _cases(int(os.environ.get("F16_FUZZ_CASES", "64")))
 
 
 def _np(x):
@@ -123,7 +128,9 @@ def test_fuzz_layouts_and_oracle(gpu, case):
         # contiguous vs the oracle
         np.testing.assert_array_equal(te_a, te_r, err_msg="terminated vs oracle @%d" % t)
         np.testing.assert_array_equal(tr_a, tr_r, err_msg="truncated vs oracle @%d" % t)
-        np.testing.assert_allclose(_np(sa.rew), rw_r, atol=2e-3, err_msg="reward vs oracle @%d" % t)
+        # the reward tolerance the frame tolerance in force implies (tests/reward_bound.py)
+        np.testing.assert_allclose(_np(sa.rew), rw_r, atol=reward_atol(TOL_RAND30 * (10 if c["cfg5"] else 1)),
+                                   err_msg="reward vs oracle @%d" % t)
         if d.any():
             finished += int(d.sum())
             np.testing.assert_array_equal(_np(sa.ep_len)[d], elen_r[d])
