@@ -324,6 +324,14 @@ int main(int argc, char** argv) {
   timed("empty_step_lds", launches, [&](hipEvent_t a, hipEvent_t b) {
     hipExtLaunchKernelGGL(k_empty_lds, dim3(g1), dim3(BLOCK), (uint32_t)step_lds, 0, a, b, 0u, (float*)nullptr);
   }, extra);
+  // round 6: does the empty launch's cost scale with the LDS a workgroup asks for?
+  for (int kb : {8, 16, 30, 46, 64, 96}) {
+    char nm[40];
+    snprintf(nm, sizeof nm, "empty_lds_%dk", kb);
+    timed(nm, launches, [&](hipEvent_t a, hipEvent_t b) {
+      hipExtLaunchKernelGGL(k_empty_lds, dim3(g1), dim3(BLOCK), (uint32_t)(kb * 1024), 0, a, b, 0u, (float*)nullptr);
+    }, extra);
+  }
   const double bytes = (double)n * (272 + 390);
   auto copy_line = [&](const char* nm, int lpe, auto kern) {
     const unsigned g = (unsigned)((n * lpe + BLOCK - 1) / BLOCK);
