@@ -323,19 +323,26 @@ __device__ __forceinline__ void lane_unpack(const float4 (&c)[NCOL], float4 w, f
     L.wind[j] = L.wst[j] + L.gust[j];
   }
 }
+// the lane's raw columns (and the wind columns of GUST handles), loads only: callers that want
+// every load of their prologue in flight before the first use unpack after their own wait
 template <bool GUST = false>
-__device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
+__device__ __forceinline__ void lane_fetch(const SoA& s, int64_t k, float4 (&c)[NCOL], float4& w, float4& g) {
   const int64_t n = s.n;
-  float4 c[NCOL];
   // column pointers by increment (one 64-bit scalar add per column, not a 64-bit multiply)
   const float4* p = s.c + k;
 #pragma unroll
   for (int j = 0; j < NCOL; ++j, p += n) c[j] = *p;
-  float4 w = make_float4(0.f, 0.f, 0.f, 0.f), g = w;
+  w = make_float4(0.f, 0.f, 0.f, 0.f);
+  g = w;
   if (GUST) {
     w = *p;
     g = *(p + n);
   }
+}
+template <bool GUST = false>
+__device__ __forceinline__ void lane_load(const SoA& s, int64_t k, Lane& L) {
+  float4 c[NCOL], w, g;
+  lane_fetch<GUST>(s, k, c, w, g);
   lane_unpack<GUST>(c, w, g, L);
 }
 // the one-env IC template staged in LDS (columns contiguous): no vector-memory traffic, so

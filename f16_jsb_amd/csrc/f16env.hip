@@ -553,7 +553,14 @@ __device__ __forceinline__ void stage_tables_issue(float* sT) {
   constexpr int NP = F16_BLOB_FLOATS / 4;  // 16-byte pieces (the generator pads the blob)
   static_assert(F16_BLOB_FLOATS % 4 == 0, "blob must be whole 16-byte pieces");
   const int wave_base = threadIdx.x & ~63;
+  // stride BLOCK, not blockDim.x: every kernel that stages the tables launches BLOCK threads, and
+  // blockDim.x is a load from the implicit kernel arguments -- the wait for it held the DMA (and
+  // the state loads behind it) until the whole argument block had arrived
+#ifdef F16_STAGE_BLOCKDIM  // (round 5's form, for the same-box A/B)
   for (int r = 0; r < NP; r += blockDim.x) {
+#else
+  for (int r = 0; r < NP; r += BLOCK) {
+#endif
     const int piece = r + threadIdx.x;
     if (piece < NP) dma16(F16_BLOB_INIT + 4 * piece, sT + 4 * (r + wave_base));
   }
@@ -770,17 +777,27 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   if (!DEFER && threadIdx.x < NCOL + TMPL_FRAME_COLS)
     dma16(reinterpret_cast<const float*>((pre ? pre->tmpl : a.tmpl.c) + (threadIdx.x < NCOL ? threadIdx.x : threadIdx.x + NCOL_ALL - NCOL)),
           reinterpret_cast<float*>(sTmpl));
+  // (the columns are unpacked after the wait, behind a scheduling barrier: a first use the
+  // scheduler hoists between the loads puts a vmcnt(0) there -- the table DMA and the first two
+  // columns' round trip, then the other fourteen's. Unconditional loads -- a lane past the end
+  // reading env 0 -- let the argument fetches issue before the wait too, but measured no faster
+  // at 65 536 envs and 0.5 us slower for cfg5's two-wave kernel: profiles/r06_ab_prologue.json)
+  float4 cl[NCOL], wl, gl;
   if (live) {
     if (pre) {
       const SoA sp = {const_cast<float4*>(pre->sc), pre->n};
-      lane_load<GUST>(sp, k, L);
+      lane_fetch<GUST>(sp, k, cl, wl, gl);
       if (!SAMPLE || !a.sample_act) av = reinterpret_cast<const float4*>(pre->act)[k];
     } else {
-      lane_load<GUST>(a.s, k, L);
+      lane_fetch<GUST>(a.s, k, cl, wl, gl);
       if (!SAMPLE || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef F16_PROLOGUE_NO_SCHED_BARRIER  // (for the same-box A/B)
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+  if (live) lane_unpack<GUST>(cl, wl, gl, L);
   __syncthreads();
   issue_stack_dma();
   if (SAMPLE && a.sample_act && live) av = philox_action(a.act_seed, (uint64_t)(a.E.id_base + k), a.act_step);

@@ -324,6 +324,14 @@ int main(int argc, char** argv) {
   timed("empty_step_lds", launches, [&](hipEvent_t a, hipEvent_t b) {
     hipExtLaunchKernelGGL(k_empty_lds, dim3(g1), dim3(BLOCK), (uint32_t)step_lds, 0, a, b, 0u, (float*)nullptr);
   }, extra);
+  // ... and which part of it is the LDS: the argument-free kernel given 46 KB, the kernel that
+  // reads its argument given none
+  timed("empty_noarg_lds_46k", launches, [&](hipEvent_t a, hipEvent_t b) {
+    hipExtLaunchKernelGGL(k_empty, dim3(g1), dim3(BLOCK), (uint32_t)step_lds, 0, a, b, 0u);
+  }, extra);
+  timed("empty_arg_nolds", launches, [&](hipEvent_t a, hipEvent_t b) {
+    hipExtLaunchKernelGGL(k_empty_lds, dim3(g1), dim3(BLOCK), 0u, 0, a, b, 0u, (float*)nullptr);
+  }, extra);
   // round 6: does the empty launch's cost scale with the LDS a workgroup asks for?
   for (int kb : {8, 16, 30, 46, 64, 96}) {
     char nm[40];
