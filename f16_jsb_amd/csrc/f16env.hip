@@ -537,6 +537,23 @@ __device__ __forceinline__ void earth_angle(double epa, double& ce, double& se) 
 #define IMG_OFF 0
 #endif
 
+// Wait for every outstanding vector-memory operation (s_waitcnt vmcnt(0)) as the compiler's
+// own wait: its wait-insertion pass then knows the LDS-DMA issued before is retired. (An
+// inline-asm s_waitcnt is opaque to that pass: it kept treating the fresh-frame DMA into the
+// staging area as pending and put another vmcnt(0) before the slot staging's LDS writes --
+// which on CDNA also waits for every state store issued in between.) The empty asm statements
+// keep the compiler from moving memory operations across it.
+#ifdef F16_ASM_VMCNT  // (round 5's form, for the same-box A/B)
+#define VM_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define VM_DRAIN()                          \
+  do {                                      \
+    asm volatile("" ::: "memory");          \
+    __builtin_amdgcn_s_waitcnt(0x0F70);     \
+    asm volatile("" ::: "memory");          \
+  } while (0)
+#endif
+
 // LDS-DMA of 16 B per lane: lane i's 16 bytes land at lds + 16*i (gfx950 global_load_lds_dwordx4)
 __device__ __forceinline__ void dma16(const float* g, float* lds) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
@@ -567,7 +584,7 @@ __device__ __forceinline__ void stage_tables_issue(float* sT) {
 }
 __device__ __forceinline__ void stage_tables(float* sT) {
   stage_tables_issue(sT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  VM_DRAIN();
   __syncthreads();
 }
 
@@ -793,7 +810,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
       if (!SAMPLE || !a.sample_act) av = reinterpret_cast<const float4*>(a.act)[k];
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  VM_DRAIN();
 #ifndef F16_PROLOGUE_NO_SCHED_BARRIER  // (for the same-box A/B)
   __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -878,7 +895,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // a lane reset by the step stores its row twice (r02_variants_early_store.txt).
   const bool early_store = LOWREG && !a.done_idx;
   if (early_store) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    VM_DRAIN();
     if (live) lane_store<GUST, 1, NT>(a.s, k, L);
   }
   if (live) {
@@ -894,7 +911,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, float* sT_lds, floa
   // the stack DMA issued after the prologue has long landed; retire it here, before any
   // store of this step (vmcnt also counts stores on CDNA, so a later wait would drain them)
   // -- unless the early state store above already did
-  if (!early_store) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!early_store) VM_DRAIN();
   // compaction of finished lanes (wave64 ballot), before any store of this step so the
   // atomic's return waits on nothing else
   if (a.done_idx) {  // (always set in deferred modes: the handle's own list if the caller gave none)
@@ -1497,7 +1514,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void f16_rollout_kernel(RollArgs a) {
 #pragma unroll
     for (int c = 0; c < F16_OBS_DIM; ++c) fn[c] = op[c];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  VM_DRAIN();
   __syncthreads();
   if (!live) return;  // no barrier below
   const int wave = tid >> 6, lane = tid & 63;
@@ -1656,7 +1673,7 @@ __global__ __launch_bounds__(BLOCK) void f16_reset_done_kernel(ResetDoneArgs a) 
   const int64_t i0 = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const int nd = *a.n_done;
   const int32_t k0 = i0 < a.E.n ? a.done_idx[i0] : -1;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  VM_DRAIN();
   __syncthreads();
   if ((int64_t)blockIdx.x * BLOCK >= nd) return;  // after the only barrier
   for (int64_t i = i0; i < nd; i += (int64_t)gridDim.x * BLOCK) {
