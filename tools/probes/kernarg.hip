@@ -99,6 +99,38 @@ __global__ __launch_bounds__(BLOCK, 1) void k_chain_glob(int buf, float* out) {
   if (acc == 12345.0f) out[i] = acc;
 }
 
+// the step's real pattern: the action pointer is an argument too; chain_glob_act issues the
+// state loads from the __device__ address, then reads the action pointer argument and loads
+// through it (the argument round trip under the state loads'); chain_arg_act reads everything
+// from the arguments first
+__global__ __launch_bounds__(BLOCK, 1) void k_chain_arg_act(const float4* st, const float4* act, int64_t n, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  float acc = 0.0f;
+  const float4* p = st + i;
+  float4 c[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j, p += n) c[j] = *p;
+  const float4 a = act[i];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc += c[j].x + c[j].w;
+  acc += a.y;
+  if (acc == 12345.0f) out[i] = acc;
+}
+__global__ __launch_bounds__(BLOCK, 1) void k_chain_glob_act(const float4* act, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t n = g_n;
+  float acc = 0.0f;
+  const float4* p = g_states[0] + i;
+  float4 c[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j, p += n) c[j] = *p;
+  const float4 a = act[i];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc += c[j].x + c[j].w;
+  acc += a.y;
+  if (acc == 12345.0f) out[i] = acc;
+}
+
 template <class F>
 static void timed(const char* name, int launches, F launch) {
   hipEvent_t s, e;
@@ -160,6 +192,15 @@ int main(int argc, char** argv) {
     });
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_states), &bufs[0], sizeof(float4*)));
     timed("chain_glob_same", launches, [&] { hipLaunchKernelGGL(k_chain_glob, grid, blk, 0, 0, 0, out); });
+    // interleaved A B A B ..., 6 pairs: the action-pointer chain both ways
+    for (int r = 0; r < 6; ++r) {
+      timed("chain_arg_act", launches, [&] {
+        hipLaunchKernelGGL(k_chain_arg_act, grid, blk, 0, 0, (const float4*)bufs[0], (const float4*)in, n, out);
+      });
+      timed("chain_glob_act", launches, [&] {
+        hipLaunchKernelGGL(k_chain_glob_act, grid, blk, 0, 0, (const float4*)in, out);
+      });
+    }
     for (int b = 0; b < NBUF; ++b) CK(hipFree(bufs[b]));
   }
   timed("empty_again", launches, [&] { hipLaunchKernelGGL(k_empty, grid, blk, 0, 0); });
