@@ -199,3 +199,39 @@ def test_packed_pairs_and_sgpr_spill_lanes(debug):
 def build_lib(debug):
     from f16_jsb_amd.build import build
     return build(debug=debug)
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="ROCm llvm-objdump not present")
+def test_step_prologue_issues_its_loads_before_any_wait():
+    """Round 6 ("The step's prologue"): past the argument-preload entry, the headline
+    step kernels issue the table LDS-DMA and all 16 state-column loads before their first
+    s_waitcnt. The kernel-argument round trip (~1 us per launch) then overlaps the state's instead
+    of preceding it; round 5's code waited for the whole argument block first (the table staging
+    strode by blockDim.x, an implicit-argument load), 0.65 us per step at 65 536 envs."""
+    asm = _disassemble(build_lib(False))
+    # (the headline kernel only: cfg5's 256-register <3, 2> build and the rollout-slot build still
+    # wait once before their state loads -- two EnvArgs fields they load up front are spilled to
+    # VGPR lanes at once, and the spill needs the value; measured neutral to remove for the
+    # rollout slot's action-flag read, profiles/r06_ab_action_pointer.json)
+    want = {"_Z22f16_step_win_nt_kernelILi0ELi1ELb0EEvPK15HIP_vector_typeIfLj4EEPKfS3_l8StepArgs": "cfg3 headline"}
+    seen = set()
+    for kernel, body in _kernels(asm):
+        if kernel not in want:
+            continue
+        seen.add(kernel)
+        # the compatibility prologue (argument loads for firmware without preload) ends in the
+        # first s_branch; the preloaded entry follows it
+        i = next(j for j, ln in enumerate(body) if ln.startswith("s_branch"))
+        dma = state = 0
+        for ln in body[i + 1:]:
+            if ln.startswith("global_load_lds_dwordx4"):
+                dma += 1
+            elif ln.startswith("global_load_dwordx4"):
+                state += 1
+                if state == 16:
+                    break
+            elif ln.startswith("s_waitcnt") or ln.startswith("s_barrier"):
+                pytest.fail("%s: %r before the 16 state loads (%d issued, %d table DMAs)"
+                            % (want[kernel], ln, state, dma))
+        assert state == 16 and dma >= 1, (want[kernel], state, dma)
+    assert seen == set(want), sorted(set(want) - seen)
