@@ -44,6 +44,7 @@ def main(path):
     dev = torch.device("cuda", 0)
 
     def steps(tag, e, n_steps, seed):
+        print("phase", tag, flush=True)  # (the last phase printed names the section of a failure)
         rew, fl = [], []
         for t in range(n_steps):
             o = e.step(e.sample_actions(seed, t))
@@ -82,6 +83,7 @@ def main(path):
 
     for layout in ("window", "contiguous"):
         for cfg5 in (False, True):
+            print("phase roll_%s%s" % (layout, "_cfg5" if cfg5 else ""), flush=True)
             e = F16Envs(n, stack_k=4, seed=8, max_steps=12, cfg5=cfg5, obs_layout=layout)
             e.reset() if cfg5 else e.reset(ic=crash_ics(n))
             b = DeviceRolloutBuffer(24, n, 4, dev)
@@ -98,6 +100,7 @@ def main(path):
             out[tag + "_features"] = features(e.obs).cpu().numpy()
             out[tag + "_poses"] = poses(e.obs).cpu().numpy()
             e.close()
+    print("phase trim", flush=True)
     e = F16Envs(256, stack_k=4, seed=9)
     ic = crash_ics(256)
     ic[:, 2] = np.linspace(3000, 30000, 256)

@@ -24,10 +24,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(lib_path, out):
-    env = dict(os.environ, F16ENV_LIB=lib_path)
+    # AMD_SERIALIZE_KERNEL=3: every launch waits for its kernel, so a device fault is reported at
+    # the call that launched the faulting kernel (and the child's last "phase" line names its
+    # section) instead of at a later synchronisation
+    env = dict(os.environ, F16ENV_LIB=lib_path, AMD_SERIALIZE_KERNEL="3")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "o1_diff_run.py"), out], env=env,
                        capture_output=True, text=True, timeout=280)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, "%s\n--- stdout tail:\n%s\n--- stderr tail:\n%s" % (
+        os.path.basename(lib_path), r.stdout[-600:], r.stderr[-3000:])
     return dict(np.load(out))
 
 
